@@ -1,0 +1,131 @@
+/*
+ * trialign.h -- C-ABI of the MI355X-native three-sequence 3-D DP scorer.
+ *
+ * This is the drop-in boundary for the reference's one hot path: the TRIALIGN
+ * module (timmy139710/HW-Accelerator-Three-Sequence-Alignment), which maps
+ * (seqA, seqB, seqC) -> optimal 7-state affine-gap 3-D DP score.
+ *
+ *   reference interface                        replaced by
+ *   ------------------------------------------ ---------------------------------
+ *   TRIALIGN ports + parameters                tsa_score_gpu()
+ *     src/TriAlign_1cyc.v:1-22                   (lengths A_idx/B_idx/C_idx ->
+ *     (start_align pulse, A/B/C_symbol pull,      la/lb/lc; symbol pull protocol
+ *      A/B/C_idx lengths, Score, finish)          -> caller-owned byte arrays;
+ *                                                 Score/finish -> *score + rc)
+ *   PE localparams MATCH/MISMATCH/GO/GE        tsa_params + tsa_default_params()
+ *     src/PE_1cyc.v:55-61 (compile-time)         (runtime; defaults = RTL values)
+ *   SCORE_BITS parameter (12)                  tsa_params.score_bits
+ *     src/TriAlign_tb.sv:56, TriAlign_1cyc.v:6
+ *   temp_ABC triple score                      tsa_params.s3_mode (RTL literal by
+ *     src/PE_1cyc.v:162                           default; sum-of-pairs optional)
+ *   testbench one-shot start/finish FSM        tsa_score_batch(): many triples,
+ *     src/TriAlign_tb.sv:279-333                  sharded over the node's GPUs
+ *   (no reference equivalent: the reference    tsa_score_batch_async(): device
+ *    has one alignment in flight)                 pointers + caller stream, for
+ *                                                 in-HBM throughput runs
+ *
+ * Conventions
+ *   - Symbols are one byte each, 0..4 = A,T,C,G,N (src/TriAlign_tb.sv:42-46).
+ *     Values > 4 -> TSA_EINVAL. Symbols are reduced mod 4 exactly as the 2-bit
+ *     PE symbol registers do (src/PE_1cyc.v:63-66), so N aliases A.
+ *   - Lengths >= 1. There is no RTL length envelope here (multiples of 8,
+ *     LB <= LA <= 512): results outside it follow the recurrence.
+ *   - Return 0 (TSA_OK) or a negative TSA_E* code. Functions are thread-safe
+ *     and retain no caller pointer. GPU calls other than *_async are
+ *     synchronous.
+ *   - Every GPU entry point fails with TSA_ENODEV when no HIP device is
+ *     present: there is no CPU fallback in this library.
+ */
+#ifndef TRIALIGN_H
+#define TRIALIGN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSA_OK 0
+#define TSA_EINVAL (-1)    /* bad pointer, length, symbol or parameter        */
+#define TSA_ERANGE (-2)    /* score range cannot be represented exactly       */
+#define TSA_ENODEV (-3)    /* no HIP device / device index out of range       */
+#define TSA_EDEVICE (-4)   /* HIP runtime error                               */
+#define TSA_ENOMEM (-5)    /* device allocation failed / workspace too small  */
+#define TSA_EINTERNAL (-6) /* kernel self-check failed                        */
+
+#define TSA_S3_RTL 0 /* temp_ABC as the RTL evaluates it (src/PE_1cyc.v:162) */
+#define TSA_S3_SOP 1 /* sum of the three pair scores                          */
+
+/* Kernel selection for tsa_score_*; TSA_KERNEL_AUTO picks per shape. */
+#define TSA_KERNEL_AUTO 0
+#define TSA_KERNEL_PLANE 1  /* anti-diagonal plane sweep, literal RTL arithmetic */
+#define TSA_KERNEL_PENCIL 2 /* register-systolic pencil sweep (factored form)    */
+
+typedef struct tsa_params {
+  int32_t match;      /* MATCH      (src/PE_1cyc.v:55), default  1 */
+  int32_t mismatch;   /* MISMATCH   (src/PE_1cyc.v:56), default -1 */
+  int32_t gap_open;   /* GO         (src/PE_1cyc.v:57), default  2 */
+  int32_t gap_extend; /* GE         (src/PE_1cyc.v:58), default  1 */
+  int32_t s3_mode;    /* TSA_S3_RTL (default) or TSA_S3_SOP          */
+  int32_t score_bits; /* 12 = RTL SCORE_BITS wrap (default); 0 = no wrap;
+                         13..16 also accepted                         */
+} tsa_params;
+
+/* Fill *p with the RTL's effective constants (1, -1, 2, 1, RTL s3, 12 bits). */
+void tsa_default_params(tsa_params *p);
+
+/* Host-side validation of one triple + params (no device work). */
+int tsa_validate(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
+                 const uint8_t *c, int32_t lc, const tsa_params *p);
+
+/* Score one triple on HIP device `device` (synchronous). Host buffers.
+ * final_states (nullable) receives the 7 states {M,Ix,Iy,Iz,Ixy,Iyz,Ixz} of
+ * cell (la,lb,lc) -- the 84-bit SRAM word of src/TriAlign_1cyc.v:130,138 --
+ * and is only filled by the PLANE kernel (TSA_KERNEL_PLANE); other kernels
+ * leave it untouched. */
+int tsa_score_gpu(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
+                  const uint8_t *c, int32_t lc, const tsa_params *p,
+                  int32_t *score, int32_t device);
+
+/* As tsa_score_gpu with an explicit kernel choice and optional final states. */
+int tsa_score_gpu_ex(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
+                     const uint8_t *c, int32_t lc, const tsa_params *p,
+                     int32_t kernel, int32_t *score, int32_t *final_states,
+                     int32_t device);
+
+/* Score n independent triples held back to back in host memory:
+ * triple i is seqs[offsets[3i] .. offsets[3i+1]) = A,
+ * [offsets[3i+1] .. offsets[3i+2]) = B, [offsets[3i+2] .. offsets[3i+3]) = C.
+ * offsets has 3n+1 entries. Triples are sharded over min(n_devices, visible
+ * devices) GPUs (n_devices <= 0: all visible), one host thread per device. */
+int tsa_score_batch(const uint8_t *seqs, const int64_t *offsets, int32_t n,
+                    const tsa_params *p, int32_t *scores, int32_t n_devices);
+
+/* Device-resident batch. d_seqs/d_offsets/d_scores are device pointers on the
+ * current device; stream is a hipStream_t (NULL = default stream). The
+ * workspace must hold tsa_batch_workspace_size() bytes. max_l* bound every
+ * triple's lengths. Launches only; no host synchronisation. Validation of
+ * symbols is the caller's job on this path (tsa_validate on the host copy). */
+int tsa_batch_workspace_size(int32_t n, int32_t max_la, int32_t max_lb,
+                             int32_t max_lc, const tsa_params *p,
+                             int32_t kernel, size_t *bytes);
+int tsa_score_batch_async(const uint8_t *d_seqs, const int64_t *d_offsets,
+                          int32_t n, int32_t max_la, int32_t max_lb,
+                          int32_t max_lc, const tsa_params *p, int32_t kernel,
+                          int32_t *d_scores, void *d_workspace,
+                          size_t workspace_bytes, void *stream);
+
+/* Number of visible HIP devices (0 when none), or a negative code. */
+int tsa_device_count(void);
+
+/* Short description of a return code. */
+const char *tsa_strerror(int rc);
+
+/* Library build id, e.g. "trialign-mi355x gfx950 <git-describe>". */
+const char *tsa_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TRIALIGN_H */
