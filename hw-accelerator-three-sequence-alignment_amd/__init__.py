@@ -1,0 +1,310 @@
+"""trialign-mi355x host API: Python mirror of the reference's TRIALIGN boundary.
+
+The reference exposes one operator: the ``TRIALIGN`` module
+(``src/TriAlign_1cyc.v:1-22``) -- parameters ``A/B/C_TOTAL_LEN, PE_LEN,
+SCORE_BITS, SRAM_ADDR_BITS``; a ``start_align`` pulse; sequence lengths on
+``A_idx/B_idx/C_idx``; symbols pulled through ``A/B/C_addr``/``*_symbol``; and
+``Score``/``finish`` out. Its only caller is the testbench FSM
+(``src/TriAlign_tb.sv:279-353``), which prints ``TriAlign Score: <n>``.
+
+This module keeps that shape (:class:`TriAlign` with the same parameter names
+and a ``run`` that plays start->finish) over the C-ABI in ``include/trialign.h``
+(``lib/libtrialign.so``, HIP/gfx950). There is no CPU fallback: if the shared
+library is missing, importing this module raises; on a host without a GPU every
+scoring call raises :class:`TsaError` with ``TSA_ENODEV``.
+
+Load it with :func:`load` from the repo root helpers, or::
+
+    spec = importlib.util.spec_from_file_location(
+        "tsa_amd", "<repo>/hw-accelerator-three-sequence-alignment_amd/__init__.py")
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libtrialign.so")
+
+TSA_OK = 0
+TSA_EINVAL = -1
+TSA_ERANGE = -2
+TSA_ENODEV = -3
+TSA_EDEVICE = -4
+TSA_ENOMEM = -5
+TSA_EINTERNAL = -6
+
+S3_RTL = 0
+S3_SOP = 1
+
+KERNEL_AUTO = 0
+KERNEL_PLANE = 1
+KERNEL_PENCIL = 2
+KERNELS = {"auto": KERNEL_AUTO, "plane": KERNEL_PLANE, "pencil": KERNEL_PENCIL}
+
+# testbench symbol encoding, src/TriAlign_tb.sv:42-46
+SYMBOLS = {"A": 0, "T": 1, "C": 2, "G": 3, "N": 4}
+
+# The C-ABI entry points include/trialign.h declares (checked by the tests).
+EXPORTS = (
+    "tsa_default_params", "tsa_validate", "tsa_score_gpu", "tsa_score_gpu_ex",
+    "tsa_score_batch", "tsa_batch_workspace_size", "tsa_score_batch_async",
+    "tsa_device_count", "tsa_strerror", "tsa_version",
+)
+
+
+class TsaParams(ctypes.Structure):
+    """``tsa_params`` (include/trialign.h); defaults = PE localparams
+    MATCH=1, MISMATCH=-1, GO=2, GE=1 (src/PE_1cyc.v:55-58), RTL s3,
+    SCORE_BITS=12 (src/TriAlign_tb.sv:56)."""
+
+    _fields_ = [
+        ("match", ctypes.c_int32),
+        ("mismatch", ctypes.c_int32),
+        ("gap_open", ctypes.c_int32),
+        ("gap_extend", ctypes.c_int32),
+        ("s3_mode", ctypes.c_int32),
+        ("score_bits", ctypes.c_int32),
+    ]
+
+    @classmethod
+    def default(cls, **kw) -> "TsaParams":
+        p = cls(1, -1, 2, 1, S3_RTL, 12)
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+    def as_tuple(self):
+        return tuple(getattr(self, f) for f, _ in self._fields_)
+
+
+class TsaError(RuntimeError):
+    def __init__(self, rc: int, what: str = ""):
+        self.rc = rc
+        msg = _lib.tsa_strerror(rc).decode() if _lib is not None else str(rc)
+        super().__init__(f"{what}: {msg} ({rc})" if what else f"{msg} ({rc})")
+
+
+def _load_lib() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libtrialign.so not built ({LIB_PATH}); run `make` or __graft_entry__.build()")
+    lib = ctypes.CDLL(LIB_PATH)
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    i64p = ctypes.POINTER(ctypes.c_int64)
+    pp = ctypes.POINTER(TsaParams)
+    lib.tsa_default_params.argtypes = [pp]
+    lib.tsa_default_params.restype = None
+    lib.tsa_validate.argtypes = [u8p, ctypes.c_int32, u8p, ctypes.c_int32, u8p, ctypes.c_int32, pp]
+    lib.tsa_score_gpu.argtypes = [u8p, ctypes.c_int32, u8p, ctypes.c_int32, u8p, ctypes.c_int32,
+                                  pp, i32p, ctypes.c_int32]
+    lib.tsa_score_gpu_ex.argtypes = [u8p, ctypes.c_int32, u8p, ctypes.c_int32, u8p,
+                                     ctypes.c_int32, pp, ctypes.c_int32, i32p, i32p,
+                                     ctypes.c_int32]
+    lib.tsa_score_batch.argtypes = [u8p, i64p, ctypes.c_int32, pp, i32p, ctypes.c_int32]
+    lib.tsa_batch_workspace_size.argtypes = [ctypes.c_int32] * 4 + [pp, ctypes.c_int32,
+                                                                   ctypes.POINTER(ctypes.c_size_t)]
+    lib.tsa_score_batch_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
+                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, pp,
+                                          ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_size_t, ctypes.c_void_p]
+    lib.tsa_device_count.argtypes = []
+    lib.tsa_strerror.argtypes = [ctypes.c_int]
+    lib.tsa_strerror.restype = ctypes.c_char_p
+    lib.tsa_version.argtypes = []
+    lib.tsa_version.restype = ctypes.c_char_p
+    for name in ("tsa_validate", "tsa_score_gpu", "tsa_score_gpu_ex", "tsa_score_batch",
+                 "tsa_batch_workspace_size", "tsa_score_batch_async", "tsa_device_count"):
+        getattr(lib, name).restype = ctypes.c_int
+    return lib
+
+
+_lib: Optional[ctypes.CDLL] = None
+_lib = _load_lib()
+
+
+def lib() -> ctypes.CDLL:
+    return _lib
+
+
+def version() -> str:
+    return _lib.tsa_version().decode()
+
+
+def device_count() -> int:
+    return int(_lib.tsa_device_count())
+
+
+def _as_u8(seq) -> np.ndarray:
+    if isinstance(seq, str):
+        try:
+            seq = [SYMBOLS[ch] for ch in seq.upper()]
+        except KeyError as e:
+            raise TsaError(TSA_EINVAL, f"symbol {e}") from None
+    arr = np.ascontiguousarray(np.asarray(seq, dtype=np.uint8))
+    if arr.ndim != 1:
+        raise TsaError(TSA_EINVAL, "sequence must be 1-D")
+    return arr
+
+
+def _ptr(arr: np.ndarray, ctype):
+    return arr.ctypes.data_as(ctypes.POINTER(ctype))
+
+
+def _check(rc: int, what: str):
+    if rc != TSA_OK:
+        raise TsaError(rc, what)
+
+
+def validate(a, b, c, params: Optional[TsaParams] = None) -> int:
+    """tsa_validate: returns the rc (0 = ok) without raising."""
+    p = params or TsaParams.default()
+    A, B, C = _as_u8(a), _as_u8(b), _as_u8(c)
+    return int(_lib.tsa_validate(_ptr(A, ctypes.c_uint8), len(A), _ptr(B, ctypes.c_uint8), len(B),
+                                 _ptr(C, ctypes.c_uint8), len(C), ctypes.byref(p)))
+
+
+def score(a, b, c, params: Optional[TsaParams] = None, kernel: str | int = "auto",
+          device: int = 0, final_states: bool = False):
+    """Optimal 3-D DP score of one triple on GPU ``device``.
+
+    ``final_states=True`` also returns the 7 states {M,Ix,Iy,Iz,Ixy,Iyz,Ixz}
+    of cell (LA,LB,LC) (runs the plane kernel)."""
+    p = params or TsaParams.default()
+    A, B, C = _as_u8(a), _as_u8(b), _as_u8(c)
+    k = KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
+    out = ctypes.c_int32(0)
+    fin = (ctypes.c_int32 * 7)()
+    rc = _lib.tsa_score_gpu_ex(_ptr(A, ctypes.c_uint8), len(A), _ptr(B, ctypes.c_uint8), len(B),
+                               _ptr(C, ctypes.c_uint8), len(C), ctypes.byref(p), k,
+                               ctypes.byref(out), fin if final_states else None, device)
+    _check(rc, "tsa_score_gpu_ex")
+    if final_states:
+        return int(out.value), tuple(int(v) for v in fin)
+    return int(out.value)
+
+
+def pack_batch(triples: Iterable[Sequence]) -> tuple[np.ndarray, np.ndarray]:
+    """Lay triples out back to back as tsa_score_batch expects."""
+    parts, offs, pos = [], [0], 0
+    for (a, b, c) in triples:
+        for s in (a, b, c):
+            arr = _as_u8(s)
+            parts.append(arr)
+            pos += len(arr)
+            offs.append(pos)
+    seqs = np.concatenate(parts) if parts else np.zeros(1, np.uint8)
+    return np.ascontiguousarray(seqs), np.asarray(offs, dtype=np.int64)
+
+
+def score_batch(triples=None, params: Optional[TsaParams] = None, n_devices: int = 0,
+                seqs: Optional[np.ndarray] = None, offsets: Optional[np.ndarray] = None) -> np.ndarray:
+    """Scores of many triples, sharded over the node's GPUs (tsa_score_batch)."""
+    p = params or TsaParams.default()
+    if seqs is None:
+        seqs, offsets = pack_batch(triples)
+    seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    n = (len(offsets) - 1) // 3
+    out = np.zeros(max(n, 1), dtype=np.int32)
+    rc = _lib.tsa_score_batch(_ptr(seqs, ctypes.c_uint8), _ptr(offsets, ctypes.c_int64), n,
+                              ctypes.byref(p), _ptr(out, ctypes.c_int32), n_devices)
+    _check(rc, "tsa_score_batch")
+    return out[:n]
+
+
+def workspace_size(n: int, max_la: int, max_lb: int, max_lc: int,
+                   params: Optional[TsaParams] = None, kernel: str | int = "auto") -> int:
+    p = params or TsaParams.default()
+    k = KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
+    sz = ctypes.c_size_t(0)
+    _check(_lib.tsa_batch_workspace_size(n, max_la, max_lb, max_lc, ctypes.byref(p), k,
+                                         ctypes.byref(sz)), "tsa_batch_workspace_size")
+    return int(sz.value)
+
+
+def score_batch_async(d_seqs_ptr: int, d_offsets_ptr: int, n: int, max_la: int, max_lb: int,
+                      max_lc: int, d_scores_ptr: int, d_ws_ptr: int, ws_bytes: int,
+                      stream_ptr: int = 0, params: Optional[TsaParams] = None,
+                      kernel: str | int = "auto") -> None:
+    """Device-resident batch (tsa_score_batch_async). Pointers are raw device
+    addresses (e.g. ``tensor.data_ptr()``), stream a hipStream_t handle."""
+    p = params or TsaParams.default()
+    k = KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
+    rc = _lib.tsa_score_batch_async(ctypes.c_void_p(d_seqs_ptr), ctypes.c_void_p(d_offsets_ptr),
+                                    n, max_la, max_lb, max_lc, ctypes.byref(p), k,
+                                    ctypes.c_void_p(d_scores_ptr), ctypes.c_void_p(d_ws_ptr),
+                                    ctypes.c_size_t(ws_bytes), ctypes.c_void_p(stream_ptr))
+    _check(rc, "tsa_score_batch_async")
+
+
+def read_sequence(path: str) -> np.ndarray:
+    """dat (one decimal symbol per line, CRLF tolerant -- dat/A_seq.dat) or
+    FASTA (A=0 T=1 C=2 G=3 N=4, src/TriAlign_tb.sv:42-46)."""
+    with open(path, "r") as f:
+        text = f.read()
+    body = text.lstrip()
+    if body.startswith(">"):
+        lines = body.splitlines()[1:]
+        seq = []
+        for ln in lines:
+            if ln.startswith(">"):
+                break
+            for ch in ln.strip().upper():
+                if ch == "U":
+                    ch = "T"
+                if ch not in SYMBOLS:
+                    raise TsaError(TSA_EINVAL, f"FASTA symbol {ch!r}")
+                seq.append(SYMBOLS[ch])
+        return np.asarray(seq, dtype=np.uint8)
+    vals = [int(t) for t in body.split()]
+    if any(v < 0 or v > 4 for v in vals):
+        raise TsaError(TSA_EINVAL, "dat symbol outside 0..4")
+    return np.asarray(vals, dtype=np.uint8)
+
+
+def rtl_envelope(la: int, lb: int, lc: int, a_total_len: int = 512, pe_len: int = 8) -> bool:
+    """True when (la,lb,lc) lies inside the RTL's operating envelope, where
+    the reference hardware would compute the same score:
+    lengths multiples of PE_LEN (src/TriAlign_1cyc.v:50-51), LA <= A_TOTAL_LEN
+    (SRAM depth, :7,492) and LB <= LA (y-face ring, :44,330-332)."""
+    return (la % pe_len == 0 and lb % pe_len == 0 and lc % pe_len == 0 and 0 < la <= a_total_len
+            and 0 < lb <= la and lc > 0)
+
+
+class TriAlign:
+    """Mirror of the ``TRIALIGN`` module (src/TriAlign_1cyc.v:1-22).
+
+    Parameters keep the RTL names; ``PE_LEN`` and ``SRAM_ADDR_BITS`` only
+    describe the envelope (the GPU has no 8x8 array or SRAM depth). ``run``
+    plays the testbench's one-shot start_align -> finish handshake
+    (src/TriAlign_tb.sv:279-333) and returns ``Score``."""
+
+    def __init__(self, A_TOTAL_LEN: int = 512, B_TOTAL_LEN: int = 512, C_TOTAL_LEN: int = 512,
+                 PE_LEN: int = 8, SCORE_BITS: int = 12, SRAM_ADDR_BITS: int = 9,
+                 params: Optional[TsaParams] = None, device: int = 0, kernel: str = "auto"):
+        self.A_TOTAL_LEN, self.B_TOTAL_LEN, self.C_TOTAL_LEN = A_TOTAL_LEN, B_TOTAL_LEN, C_TOTAL_LEN
+        self.PE_LEN, self.SCORE_BITS, self.SRAM_ADDR_BITS = PE_LEN, SCORE_BITS, SRAM_ADDR_BITS
+        self.params = params or TsaParams.default(score_bits=SCORE_BITS)
+        self.device, self.kernel = device, kernel
+        self.Score: Optional[int] = None
+        self.finish = False
+
+    def in_envelope(self, la: int, lb: int, lc: int) -> bool:
+        return (rtl_envelope(la, lb, lc, min(self.A_TOTAL_LEN, 1 << self.SRAM_ADDR_BITS),
+                             self.PE_LEN) and lb <= self.B_TOTAL_LEN and lc <= self.C_TOTAL_LEN)
+
+    def run(self, A, B, C) -> int:
+        """start_align -> ... -> finish; returns Score."""
+        self.finish = False
+        self.Score = score(A, B, C, self.params, kernel=self.kernel, device=self.device)
+        self.finish = True
+        return self.Score
+
+    def display(self) -> str:
+        """The testbench's print line (src/TriAlign_tb.sv:341)."""
+        return f"TriAlign Score:        \t{self.Score}"

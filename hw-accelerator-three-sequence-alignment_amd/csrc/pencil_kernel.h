@@ -1,0 +1,18 @@
+// pencil_kernel.h -- TSA_KERNEL_PENCIL host interface (see pencil_kernel.hip).
+#pragma once
+
+#include "tsa_internal.h"
+
+namespace tsa {
+
+// Headroom (score units) the pencil kernel's int16 lanes keep beyond the
+// a-priori value bound: message biases and penalties are applied in int16.
+constexpr int64_t PENCIL_MARGIN = 512;
+
+bool pencil_supported(const tsa_params *p);
+size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc);
+int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
+                        int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
+                        int32_t *d_scores, void *d_ws, size_t ws_bytes, hipStream_t stream);
+
+}  // namespace tsa

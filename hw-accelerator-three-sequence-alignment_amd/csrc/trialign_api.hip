@@ -1,0 +1,366 @@
+// trialign_api.hip -- the C-ABI of include/trialign.h: validation, parameter
+// expansion, device memory, kernel dispatch and multi-GPU batch sharding.
+//
+// Boundary mapping (reference file:line -> entry point) is in
+// include/trialign.h. There is deliberately no CPU scoring path here: with no
+// HIP device every scoring call returns TSA_ENODEV.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "tsa_internal.h"
+#include "pencil_kernel.h"
+
+#ifndef TSA_GIT_DESCRIBE
+#define TSA_GIT_DESCRIBE "dev"
+#endif
+
+namespace tsa {
+
+static inline int64_t wrap64(int64_t v, int bits) {
+  if (bits == 0) return v;
+  const uint64_t u = (uint64_t)v << (64 - bits);
+  return (int64_t)u >> (64 - bits);
+}
+
+static int params_ok(const tsa_params *p) {
+  if (!p) return 0;
+  if (p->s3_mode != TSA_S3_RTL && p->s3_mode != TSA_S3_SOP) return 0;
+  if (p->score_bits != 0 && (p->score_bits < 4 || p->score_bits > 16)) return 0;
+  const int32_t lim = 1 << 12;
+  if (std::abs(p->match) > lim || std::abs(p->mismatch) > lim || std::abs(p->gap_open) > lim ||
+      std::abs(p->gap_extend) > lim)
+    return 0;
+  return 1;
+}
+
+int build_kparams(const tsa_params *p, KParams *kp) {
+  if (!params_ok(p) || !kp) return TSA_EINVAL;
+  std::memset(kp, 0, sizeof(*kp));
+  const int32_t GO = p->gap_open, GE = p->gap_extend;
+  const int32_t GO2 = 2 * GO, GE2 = 2 * GE, GOGE = GO + GE;
+  const int32_t t[7][7] = {
+      {0, 0, 0, 0, 0, 0, 0},                   // M   src/PE_1cyc.v:164-170
+      {GO2, GE2, GOGE, GOGE, GOGE, GO2, GOGE}, // Ix  :172-178
+      {GO2, GOGE, GE2, GOGE, GOGE, GOGE, GO2}, // Iy  :180-186
+      {GO2, GOGE, GOGE, GE2, GO2, GOGE, GOGE}, // Iz  :188-194
+      {GO, GE, GE, GO, GE, GO, GO},            // Ixy :196-202
+      {GO, GO, GE, GE, GO, GE, GO},            // Iyz :204-210
+      {GO, GE, GO, GE, GO, GO, GE},            // Ixz :212-218
+  };
+  std::memcpy(kp->pen, t, sizeof(t));
+  const int bits = p->score_bits;
+  kp->bits = bits;
+  kp->wrap_shift = bits ? 32 - bits : 0;
+  kp->match = (int32_t)wrap64(p->match, bits);
+  kp->mismatch = (int32_t)wrap64(p->mismatch, bits);
+  // src/PE_1cyc.v:162 -- '+' binds tighter than '<<' in Verilog
+  kp->s3_eq = (int32_t)wrap64(3LL * p->match, bits);
+  kp->s3_ab = (int32_t)wrap64(2LL * ((int64_t)p->match + p->mismatch), bits);
+  kp->s3_ne = (int32_t)wrap64(3LL * p->mismatch, bits);
+  kp->s3_mode = p->s3_mode;
+  return TSA_OK;
+}
+
+Range value_bound(const tsa_params *p, int64_t la, int64_t lb, int64_t lc) {
+  KParams kp;
+  build_kparams(p, &kp);
+  const int64_t m = p->match, mm = p->mismatch;
+  int64_t s3v[3];
+  if (p->s3_mode == TSA_S3_SOP) { s3v[0] = 3 * m; s3v[1] = m + 2 * mm; s3v[2] = 3 * mm; }
+  else { s3v[0] = 3 * m; s3v[1] = 2 * (m + mm); s3v[2] = 3 * mm; }
+  const int64_t s3max = *std::max_element(s3v, s3v + 3), s3min = *std::min_element(s3v, s3v + 3);
+  const int64_t s2max = std::max(m, mm), s2min = std::min(m, mm);
+  int64_t scmax[7], scmin[7], dq[7];
+  for (int T = 0; T < 7; ++T) {
+    if (T == SM) { scmax[T] = s3max; scmin[T] = s3min; dq[T] = 3; }
+    else if (T <= SIZ) { scmax[T] = 0; scmin[T] = 0; dq[T] = 1; }
+    else { scmax[T] = s2max; scmin[T] = s2min; dq[T] = 2; }
+  }
+  // upper: best(cell) <= best(pred_T) + inc_T; a path from a zero face to q
+  // advances q by dq_T per step, so every value <= q * max_T(inc_T/dq_T)^+.
+  double gain = 0.0;
+  for (int T = 0; T < 7; ++T)
+    for (int s = 0; s < 7; ++s) gain = std::max(gain, (double)(scmax[T] - kp.pen[T][s]) / dq[T]);
+  const int64_t hi = (int64_t)std::floor(gain * (double)(la + lb + lc) + 1e-9);
+  // lower: best(cell) >= best(diag) + s3 (P[M][*] = 0) -> >= min(l)*min(0,s3min)
+  const int64_t mn = std::min(la, std::min(lb, lc));
+  const int64_t bestlo = mn * std::min<int64_t>(0, s3min);
+  int64_t drop = 0, cdrop = 0;
+  for (int T = 0; T < 7; ++T) {
+    int64_t maxp = kp.pen[T][0];
+    for (int s = 0; s < 7; ++s) {
+      maxp = std::max<int64_t>(maxp, kp.pen[T][s]);
+      cdrop = std::max<int64_t>(cdrop, kp.pen[T][s] - scmin[T]);
+    }
+    drop = std::max<int64_t>(drop, maxp - scmin[T]);
+  }
+  const int64_t statelo = std::min<int64_t>(0, bestlo - drop);
+  Range r;
+  r.lo = statelo - std::max<int64_t>(0, cdrop);
+  r.hi = std::max<int64_t>(hi, 0);
+  return r;
+}
+
+}  // namespace tsa
+
+using namespace tsa;
+
+extern "C" {
+
+void tsa_default_params(tsa_params *p) {
+  if (!p) return;
+  p->match = 1;       // src/PE_1cyc.v:55
+  p->mismatch = -1;   // :56
+  p->gap_open = 2;    // :57
+  p->gap_extend = 1;  // :58
+  p->s3_mode = TSA_S3_RTL;
+  p->score_bits = 12; // src/TriAlign_tb.sv:56
+}
+
+const char *tsa_strerror(int rc) {
+  switch (rc) {
+    case TSA_OK: return "ok";
+    case TSA_EINVAL: return "invalid argument (pointer, length, symbol or parameter)";
+    case TSA_ERANGE: return "score range not representable exactly";
+    case TSA_ENODEV: return "no HIP device";
+    case TSA_EDEVICE: return "HIP runtime error";
+    case TSA_ENOMEM: return "out of device memory / workspace too small";
+    case TSA_EINTERNAL: return "internal self-check failed";
+    default: return "unknown error";
+  }
+}
+
+const char *tsa_version(void) { return "trialign-mi355x gfx950 " TSA_GIT_DESCRIBE; }
+
+int tsa_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int tsa_validate(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb, const uint8_t *c,
+                 int32_t lc, const tsa_params *p) {
+  if (!a || !b || !c || !params_ok(p)) return TSA_EINVAL;
+  if (la < 1 || lb < 1 || lc < 1) return TSA_EINVAL;
+  for (int32_t i = 0; i < la; ++i) if (a[i] > 4) return TSA_EINVAL;
+  for (int32_t i = 0; i < lb; ++i) if (b[i] > 4) return TSA_EINVAL;
+  for (int32_t i = 0; i < lc; ++i) if (c[i] > 4) return TSA_EINVAL;
+  if (p->score_bits == 0) {  // int16 state storage must hold the unwrapped range
+    const Range r = value_bound(p, la, lb, lc);
+    if (r.lo < -32768 || r.hi > 32767) return TSA_ERANGE;
+  }
+  return TSA_OK;
+}
+
+}  // extern "C"
+
+namespace tsa {
+
+// Is the factored (pencil) arithmetic bit-identical to the literal RTL form
+// for every triple of these lengths? True when no candidate can wrap at
+// score_bits and everything fits the pencil kernel's int16 lanes.
+static bool pencil_exact(const tsa_params *p, int64_t la, int64_t lb, int64_t lc) {
+  const Range r = value_bound(p, la, lb, lc);
+  const int64_t lim_lo = p->score_bits ? -(1LL << (p->score_bits - 1)) : -32768;
+  const int64_t lim_hi = p->score_bits ? (1LL << (p->score_bits - 1)) - 1 : 32767;
+  return r.lo - PENCIL_MARGIN >= std::max<int64_t>(lim_lo, -32768) &&
+         r.hi + PENCIL_MARGIN <= std::min<int64_t>(lim_hi, 32767) && pencil_supported(p);
+}
+
+static int choose_kernel(int32_t kernel, const tsa_params *p, int64_t la, int64_t lb, int64_t lc) {
+  if (kernel == TSA_KERNEL_PLANE) return TSA_KERNEL_PLANE;
+  const bool ok = pencil_exact(p, la, lb, lc);
+  if (kernel == TSA_KERNEL_PENCIL) return ok ? TSA_KERNEL_PENCIL : -1;
+  return ok ? TSA_KERNEL_PENCIL : TSA_KERNEL_PLANE;
+}
+
+static size_t workspace_for(int kind, int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  if (kind == TSA_KERNEL_PLANE) return plane_workspace_bytes(n, max_la, max_lb, max_lc);
+  return pencil_workspace_bytes(n, max_la, max_lb, max_lc);
+}
+
+static int launch_kind(int kind, const uint8_t *d_seqs, const int64_t *d_off, int32_t n,
+                       int32_t max_la, int32_t max_lb, int32_t max_lc, const tsa_params *p,
+                       int32_t *d_scores, int32_t *d_final7, void *ws, size_t ws_bytes,
+                       hipStream_t s) {
+  KParams kp;
+  int rc = build_kparams(p, &kp);
+  if (rc) return rc;
+  if (kind == TSA_KERNEL_PLANE)
+    return plane_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp, d_scores, d_final7,
+                              ws, ws_bytes, s);
+  return pencil_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp, d_scores, ws,
+                             ws_bytes, s);
+}
+
+#define HIPCHK(x)                                   \
+  do {                                              \
+    if ((x) != hipSuccess) { rc = TSA_EDEVICE; goto done; } \
+  } while (0)
+
+// Score triples [i0, i1) of a host batch on one device (synchronous).
+static int run_host_batch_on_device(int device, const uint8_t *seqs, const int64_t *offsets,
+                                    int32_t i0, int32_t i1, const tsa_params *p, int32_t kernel,
+                                    int32_t *scores, int32_t *final7) {
+  int rc = TSA_OK;
+  const int32_t n = i1 - i0;
+  if (n <= 0) return TSA_OK;
+  int32_t max_la = 0, max_lb = 0, max_lc = 0;
+  for (int32_t i = i0; i < i1; ++i) {
+    const int64_t *o = offsets + 3 * (int64_t)i;
+    max_la = std::max<int32_t>(max_la, (int32_t)(o[1] - o[0]));
+    max_lb = std::max<int32_t>(max_lb, (int32_t)(o[2] - o[1]));
+    max_lc = std::max<int32_t>(max_lc, (int32_t)(o[3] - o[2]));
+  }
+  const int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
+  if (kind < 0) return TSA_ERANGE;
+  // chunk so the workspace stays under ~8 GiB and grid.z under 65535
+  const size_t per = workspace_for(kind, 1, max_la, max_lb, max_lc);
+  int32_t chunk = (int32_t)std::max<size_t>(1, std::min<size_t>((size_t)8 << 30, (size_t)n * per) / per);
+  chunk = std::min(chunk, std::min(n, 65535));
+  const int64_t base = offsets[3 * (int64_t)i0];
+  const int64_t nbytes = offsets[3 * (int64_t)i1] - base;
+  uint8_t *d_seqs = nullptr;
+  int64_t *d_off = nullptr;
+  int32_t *d_scores = nullptr, *d_final = nullptr;
+  void *d_ws = nullptr;
+  std::vector<int64_t> off((size_t)3 * n + 1);
+  hipStream_t s = nullptr;
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  for (size_t k = 0; k < off.size(); ++k) off[k] = offsets[3 * (int64_t)i0 + (int64_t)k] - base;
+  if (hipMalloc(&d_seqs, std::max<int64_t>(nbytes, 1)) != hipSuccess ||
+      hipMalloc(&d_off, off.size() * sizeof(int64_t)) != hipSuccess ||
+      hipMalloc(&d_scores, (size_t)n * sizeof(int32_t)) != hipSuccess ||
+      (final7 && hipMalloc(&d_final, (size_t)n * 7 * sizeof(int32_t)) != hipSuccess) ||
+      hipMalloc(&d_ws, (size_t)chunk * per) != hipSuccess) {
+    rc = TSA_ENOMEM;
+    goto done;
+  }
+  HIPCHK(hipMemcpyAsync(d_seqs, seqs + base, nbytes, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d_off, off.data(), off.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(d_ws, 0, (size_t)chunk * per, s));
+  for (int32_t c0 = 0; c0 < n && rc == TSA_OK; c0 += chunk) {
+    const int32_t cn = std::min(chunk, n - c0);
+    rc = launch_kind(kind, d_seqs, d_off + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p,
+                     d_scores + c0, d_final ? d_final + 7 * (int64_t)c0 : nullptr, d_ws,
+                     (size_t)chunk * per, s);
+  }
+  if (rc) goto done;
+  HIPCHK(hipMemcpyAsync(scores + i0, d_scores, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  if (final7)
+    HIPCHK(hipMemcpyAsync(final7 + 7 * (int64_t)i0, d_final, (size_t)n * 7 * sizeof(int32_t),
+                          hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+done:
+  if (d_seqs) (void)hipFree(d_seqs);
+  if (d_off) (void)hipFree(d_off);
+  if (d_scores) (void)hipFree(d_scores);
+  if (d_final) (void)hipFree(d_final);
+  if (d_ws) (void)hipFree(d_ws);
+  if (s) (void)hipStreamDestroy(s);
+  return rc;
+}
+
+}  // namespace tsa
+
+extern "C" {
+
+int tsa_score_gpu_ex(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb, const uint8_t *c,
+                     int32_t lc, const tsa_params *p, int32_t kernel, int32_t *score,
+                     int32_t *final_states, int32_t device) {
+  if (!score) return TSA_EINVAL;
+  if (kernel < TSA_KERNEL_AUTO || kernel > TSA_KERNEL_PENCIL) return TSA_EINVAL;
+  int rc = tsa_validate(a, la, b, lb, c, lc, p);
+  if (rc) return rc;
+  const int nd = tsa_device_count();
+  if (nd <= 0) return TSA_ENODEV;
+  if (device < 0 || device >= nd) return TSA_ENODEV;
+  std::vector<uint8_t> seqs((size_t)la + lb + lc);
+  std::memcpy(seqs.data(), a, la);
+  std::memcpy(seqs.data() + la, b, lb);
+  std::memcpy(seqs.data() + la + lb, c, lc);
+  const int64_t off[4] = {0, la, (int64_t)la + lb, (int64_t)la + lb + lc};
+  const int32_t k = final_states ? TSA_KERNEL_PLANE : kernel;
+  return run_host_batch_on_device(device, seqs.data(), off, 0, 1, p, k, score, final_states);
+}
+
+int tsa_score_gpu(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb, const uint8_t *c,
+                  int32_t lc, const tsa_params *p, int32_t *score, int32_t device) {
+  return tsa_score_gpu_ex(a, la, b, lb, c, lc, p, TSA_KERNEL_AUTO, score, nullptr, device);
+}
+
+int tsa_score_batch(const uint8_t *seqs, const int64_t *offsets, int32_t n, const tsa_params *p,
+                    int32_t *scores, int32_t n_devices) {
+  if (!seqs || !offsets || !scores || n < 0 || !params_ok(p)) return TSA_EINVAL;
+  if (n == 0) return TSA_OK;
+  for (int32_t i = 0; i < n; ++i) {
+    const int64_t *o = offsets + 3 * (int64_t)i;
+    if (o[1] < o[0] || o[2] < o[1] || o[3] < o[2]) return TSA_EINVAL;
+    int rc = tsa_validate(seqs + o[0], (int32_t)(o[1] - o[0]), seqs + o[1], (int32_t)(o[2] - o[1]),
+                          seqs + o[2], (int32_t)(o[3] - o[2]), p);
+    if (rc) return rc;
+  }
+  const int nd = tsa_device_count();
+  if (nd <= 0) return TSA_ENODEV;
+  const int use = std::max(1, std::min(n_devices <= 0 ? nd : n_devices, std::min(nd, n)));
+  std::vector<int> rcs(use, TSA_OK);
+  std::vector<std::thread> th;
+  for (int d = 0; d < use; ++d) {
+    const int32_t i0 = (int32_t)((int64_t)n * d / use), i1 = (int32_t)((int64_t)n * (d + 1) / use);
+    th.emplace_back([&, d, i0, i1] {
+      rcs[d] = run_host_batch_on_device(d, seqs, offsets, i0, i1, p, TSA_KERNEL_AUTO, scores, nullptr);
+    });
+  }
+  for (auto &t : th) t.join();
+  for (int r : rcs) if (r) return r;
+  return TSA_OK;
+}
+
+int tsa_batch_workspace_size(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
+                             const tsa_params *p, int32_t kernel, size_t *bytes) {
+  if (!bytes || n < 0 || max_la < 1 || max_lb < 1 || max_lc < 1 || !params_ok(p)) return TSA_EINVAL;
+  if (kernel < TSA_KERNEL_AUTO || kernel > TSA_KERNEL_PENCIL) return TSA_EINVAL;
+  const int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
+  if (kind < 0) return TSA_ERANGE;
+  *bytes = workspace_for(kind, n, max_la, max_lb, max_lc);
+  return TSA_OK;
+}
+
+int tsa_score_batch_async(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
+                          int32_t max_la, int32_t max_lb, int32_t max_lc, const tsa_params *p,
+                          int32_t kernel, int32_t *d_scores, void *d_workspace,
+                          size_t workspace_bytes, void *stream) {
+  if (!d_seqs || !d_offsets || !d_scores || !d_workspace || n < 0 || max_la < 1 || max_lb < 1 ||
+      max_lc < 1 || !params_ok(p))
+    return TSA_EINVAL;
+  if (kernel < TSA_KERNEL_AUTO || kernel > TSA_KERNEL_PENCIL) return TSA_EINVAL;
+  if (tsa_device_count() <= 0) return TSA_ENODEV;
+  if (p->score_bits == 0) {
+    const Range r = value_bound(p, max_la, max_lb, max_lc);
+    if (r.lo < -32768 || r.hi > 32767) return TSA_ERANGE;
+  }
+  const int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
+  if (kind < 0) return TSA_ERANGE;
+  if (workspace_bytes < workspace_for(kind, n, max_la, max_lb, max_lc)) return TSA_ENOMEM;
+  hipStream_t s = (hipStream_t)stream;
+  for (int32_t c0 = 0; c0 < n; c0 += 65535) {
+    const int32_t cn = std::min<int32_t>(65535, n - c0);
+    const size_t wsz = workspace_for(kind, cn, max_la, max_lb, max_lc);
+    int rc = launch_kind(kind, d_seqs, d_offsets + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p,
+                         d_scores + c0, nullptr, d_workspace, wsz, s);
+    if (rc) return rc;
+  }
+  return TSA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,56 @@
+// tsa_internal.h -- shared host/device definitions of the TriAlign MI355X
+// library (not part of the C-ABI; see include/trialign.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/trialign.h"
+
+namespace tsa {
+
+// State order of the RTL SRAM word {M,Ix,Iy,Iz,Ixy,Iyz,Ixz}
+// (src/TriAlign_1cyc.v:130,138).
+enum { SM = 0, SIX, SIY, SIZ, SIXY, SIYZ, SIXZ, NSTATE = 7 };
+
+// Scoring constants expanded once on the host and passed by value.
+struct KParams {
+  int32_t pen[7][7];      // P[target][source], src/PE_1cyc.v:164-218
+  int32_t match;          // temp_AB/BC/AC arms (src/PE_1cyc.v:159-161), wrapped
+  int32_t mismatch;
+  int32_t s3_eq;          // temp_ABC arms (src/PE_1cyc.v:162), wrapped:
+  int32_t s3_ab;          //   a==b==c / a==b!=c / a!=b   (RTL mode)
+  int32_t s3_ne;
+  int32_t s3_mode;        // TSA_S3_RTL / TSA_S3_SOP
+  int32_t bits;           // SCORE_BITS wrap, 0 = none
+  int32_t wrap_shift;     // 32 - bits, or 0 when bits == 0
+};
+
+// Inclusive bounds on every candidate and state value of a (la,lb,lc) cube
+// under params p (no wrap). Used to decide whether int16 storage and the
+// factored (message) form are exact.
+struct Range {
+  int64_t lo, hi;
+};
+
+int build_kparams(const tsa_params *p, KParams *kp);
+Range value_bound(const tsa_params *p, int64_t la, int64_t lb, int64_t lc);
+
+// Row stride (elements) of a (y,z) plane with lc+1 columns, padded so rows
+// start 16-byte aligned for int16 storage.
+inline int64_t plane_ldz(int64_t lc) { return ((lc + 1 + 7) / 8) * 8; }
+
+// ---- plane kernel (TSA_KERNEL_PLANE) --------------------------------------
+struct PlaneLayout {
+  int64_t ldz;          // row stride of a (y,z) plane
+  int64_t plane;        // elements per state-plane = (max_lb+1)*ldz
+  int64_t per_triple;   // elements per triple = 4 slots * 7 states * plane
+};
+PlaneLayout plane_layout(int32_t max_lb, int32_t max_lc);
+size_t plane_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc);
+int plane_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
+                       int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
+                       int32_t *d_scores, int32_t *d_final7, void *d_ws, size_t ws_bytes,
+                       hipStream_t stream);
+
+}  // namespace tsa

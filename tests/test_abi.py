@@ -1,0 +1,104 @@
+"""C-ABI library checks that need no GPU: it loads, exports exactly what
+include/trialign.h declares, and its host-only entry points behave."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import PKG_DIR, ROOT
+
+
+def header_functions():
+    with open(os.path.join(ROOT, "include", "trialign.h")) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(tsa_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_expected_entry_points(tsa):
+    assert set(header_functions()) == set(tsa.EXPORTS)
+
+
+def test_library_exports_every_header_symbol(tsa):
+    lib = os.path.join(PKG_DIR, "lib", "libtrialign.so")
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\sT\s(tsa_[a-z0-9_]+)", out))
+    for fn in header_functions():
+        assert fn in exported, fn
+        assert hasattr(tsa.lib(), fn)
+
+
+def test_library_does_not_link_the_oracle():
+    lib = os.path.join(PKG_DIR, "lib", "libtrialign.so")
+    out = subprocess.run(["nm", "-D", lib], capture_output=True, text=True, check=True).stdout
+    assert "tsao_" not in out
+    deps = subprocess.run(["ldd", lib], capture_output=True, text=True).stdout
+    assert "tsa_oracle" not in deps
+
+
+def test_default_params_are_rtl_localparams(tsa):
+    p = tsa.TsaParams()
+    tsa.lib().tsa_default_params(ctypes.byref(p))
+    assert p.as_tuple() == (1, -1, 2, 1, tsa.S3_RTL, 12)
+    assert tsa.TsaParams.default().as_tuple() == p.as_tuple()
+
+
+def test_strerror_and_version(tsa):
+    for rc in (0, -1, -2, -3, -4, -5, -6, -99):
+        assert isinstance(tsa.lib().tsa_strerror(rc), bytes)
+    assert tsa.version().startswith("trialign-mi355x gfx950")
+
+
+def test_validate(tsa):
+    ok = [0, 1, 2, 3, 4]
+    assert tsa.validate(ok, ok, ok) == tsa.TSA_OK
+    assert tsa.validate([5], ok, ok) == tsa.TSA_EINVAL          # symbol > 4
+    assert tsa.validate([], ok, ok) == tsa.TSA_EINVAL           # empty
+    assert tsa.validate(ok, ok, ok, tsa.TsaParams.default(s3_mode=7)) == tsa.TSA_EINVAL
+    assert tsa.validate(ok, ok, ok, tsa.TsaParams.default(score_bits=17)) == tsa.TSA_EINVAL
+    assert tsa.validate(ok, ok, ok, tsa.TsaParams.default(score_bits=3)) == tsa.TSA_EINVAL
+    assert tsa.validate(ok, ok, ok, tsa.TsaParams.default(score_bits=0)) == tsa.TSA_OK
+    # unbounded arithmetic whose value range cannot fit int16 state storage
+    big = tsa.TsaParams.default(match=4000, score_bits=0)
+    assert tsa.validate([0] * 20, [0] * 20, [0] * 20, big) == tsa.TSA_ERANGE
+
+
+def test_workspace_size(tsa):
+    p = tsa.TsaParams.default()
+    n1 = tsa.workspace_size(1, 64, 64, 64, p, "plane")
+    n4 = tsa.workspace_size(4, 64, 64, 64, p, "plane")
+    assert n4 == 4 * n1 and n1 >= 4 * 7 * 65 * 65 * 2
+    # O(N^2) memory: doubling N roughly quadruples the plane ring
+    n2 = tsa.workspace_size(1, 128, 128, 128, p, "plane")
+    assert 3.5 < n2 / n1 < 4.5
+    with pytest.raises(tsa.TsaError):
+        tsa.workspace_size(1, 0, 64, 64, p)
+
+
+@pytest.mark.skipif(os.environ.get("TSA_EXPECT_GPU") == "1", reason="GPU box")
+def test_no_cpu_fallback_without_gpu(tsa):
+    if tsa.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    with pytest.raises(tsa.TsaError) as e:
+        tsa.score([0, 1], [0, 1], [0, 1])
+    assert e.value.rc == tsa.TSA_ENODEV
+    with pytest.raises(tsa.TsaError) as e:
+        tsa.score_batch([([0], [1], [2])])
+    assert e.value.rc == tsa.TSA_ENODEV
+
+
+def test_cli_reports_no_device_or_score():
+    cli = os.path.join(PKG_DIR, "bin", "tsa")
+    dat = "/root/reference/dat"
+    if not os.path.isdir(dat):
+        pytest.skip("reference not mounted")
+    r = subprocess.run([cli, f"{dat}/A_seq.dat", f"{dat}/B_seq.dat", f"{dat}/C_seq.dat"],
+                       capture_output=True, text=True)
+    if r.returncode == 0:
+        assert "TriAlign Score:" in r.stdout and r.stdout.split()[-1] == "1"
+    else:
+        assert "no HIP device" in r.stderr
