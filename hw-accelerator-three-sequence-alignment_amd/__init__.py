@@ -26,6 +26,13 @@ from typing import Iterable, Optional, Sequence
 
 import numpy as np
 
+# One HIP runtime per process: torch ships its own libamdhip64 (soname
+# libamdhip64.so.7, NEEDED as "libamdhip64.so"). Importing torch first makes
+# libtrialign.so bind to that same runtime, so torch device pointers and
+# streams passed through the C-ABI are valid; loading ours first would pull a
+# second runtime from /opt/rocm and break torch's device init.
+import torch  # noqa: F401  (device memory / streams plumbing)
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libtrialign.so")
 
