@@ -10,6 +10,7 @@ namespace tsa {
 constexpr int64_t PENCIL_MARGIN = 512;
 
 bool pencil_supported(const tsa_params *p);
+bool pencil_shape_supported(int32_t max_la, int32_t max_lb, int32_t max_lc);
 size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc);
 int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                         int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,

@@ -1,22 +1,449 @@
-// pencil_kernel.hip -- TSA_KERNEL_PENCIL (placeholder until the systolic
-// pencil kernel lands; AUTO dispatch routes every shape to the plane kernel).
+// pencil_kernel.hip -- TSA_KERNEL_PENCIL: register-systolic 3-D DP for CDNA4.
+//
+// The reference computes the cube with an 8x8 systolic PE array over (y,z)
+// while A streams along x (src/TriAlign_1cyc.v:115-125, PE_1cyc.v:247-299),
+// slicing the (y,z) plane into 8x8 pencils with face SRAMs between them
+// (src/TriAlign_1cyc.v:78-98). This kernel keeps that idea -- every cell is
+// computed from neighbour values that arrive by systolic shifts, never from a
+// stored cube -- but shapes it for a 64-lane wave:
+//
+//  * one workgroup scores one triple; wave w of NW owns DP row y = lap*NW+w+1;
+//  * the 64 lanes x M packed int16 pairs own Zt = 128*M consecutive z
+//    positions k (lane l, pair i, half h -> k = l + 64h + 128i), z = k+1;
+//  * position k of wave w computes cell x = u mod P + 1 of lap u div P at step
+//    t, with u = t - w - k (one step of skew per y and per z). A lane that
+//    finishes x = P of lap L continues with x = 1 of lap L+1 (row y+NW), so
+//    there is no fill/drain between rows: the positions form a helix;
+//  * z-1 neighbours arrive by one DPP wave_ror:1 + v_perm per packed value,
+//    y-1 neighbours through a 2-slot LDS record per wave pair, and the wave
+//    above wave 0 (row y-1 of the previous lap) through a global ring that the
+//    last wave writes and wave 0 prefetches PD steps ahead with LDS-DMA;
+//  * A, B and the "x == 1" position flow through the same shifts; only lane
+//    0 of pair 0 gets injected values (the z = 0 face, the next A symbol and
+//    the current B symbol).
+//
+// Arithmetic is the factored ("message") form of src/PE_1cyc.v:164-218: a
+// cell sends to each successor target T the value max_s(S[s] - P[T][s]) and
+// the successor adds its pair/triple score. It equals the RTL's literal
+// 49-candidate MAX7 whenever no candidate wraps at SCORE_BITS and every value
+// fits int16, which the host proves a priori (trialign_api.hip:pencil_exact)
+// before it ever selects this kernel.
+//
+// Supported shapes: LC <= 128*M (M = 1 or 2), LA <= 4096, LB <= 4096.
+
+#include <algorithm>
+
 #include "pencil_kernel.h"
 
 namespace tsa {
 
-bool pencil_supported(const tsa_params *p) {
-  (void)p;
-  return false;
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int PENCIL_NW = 16;      // waves (= DP rows) per lap
+constexpr int PD = 8;              // LDS-DMA prefetch distance of wave 0, steps
+constexpr int STORE_SLACK = 4;     // last wave keeps <= this many steps of stores in flight
+constexpr int PMIN = 48;           // >= PD + NW + STORE_SLACK + margin
+constexpr int MAX_LA = 4096, MAX_LB = 4096;
+constexpr int REC_BYTES = 16;      // {Iy, Ixy, Iyz, best} packed pairs per lane
+constexpr int RING_EXTRA = 8;
+
+struct PencilArgs {
+  uint32_t E, O, E2, OE, O2;    // packed penalties GE, GO, 2GE, GO+GE, 2GO
+  uint32_t f_single, f_pair;    // face messages of an all-zero cell
+  uint32_t dm, mm;              // match-mismatch, mismatch
+  uint32_t s3_d1, s3_d0, s3_ne; // RTL: s3 = ne + eab*(d0 + ebc*d1)
+  int32_t sop;                  // TSA_S3_SOP
+};
+
+struct PencilGeom {
+  int32_t M;        // pairs per lane
+  int32_t P;        // lap period (steps)
+  int32_t R;        // ring rows
+  int64_t ring_bytes_per_triple;
+};
+
+static inline int32_t pencil_pairs(int32_t max_lc) { return max_lc <= 128 ? 1 : 2; }
+
+static PencilGeom pencil_geom(int32_t max_la, int32_t max_lc) {
+  PencilGeom g;
+  g.M = pencil_pairs(max_lc);
+  const int32_t zt = 128 * g.M;
+  g.P = std::max(std::max(max_la, zt), PMIN);
+  g.R = g.P + RING_EXTRA;
+  g.ring_bytes_per_triple = (int64_t)g.R * g.M * 64 * REC_BYTES;
+  return g;
+}
+
+bool pencil_supported(const tsa_params *p) { return p != nullptr; }
+
+static bool pencil_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  return max_la >= 1 && max_la <= MAX_LA && max_lb >= 1 && max_lb <= MAX_LB && max_lc >= 1 &&
+         max_lc <= 256;
 }
 
 size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
-  (void)n; (void)max_la; (void)max_lb; (void)max_lc;
-  return 0;
+  if (!pencil_shape_ok(max_la, max_lb, max_lc)) return 0;
+  return (size_t)n * (size_t)pencil_geom(max_la, max_lc).ring_bytes_per_triple;
 }
 
-int pencil_launch_batch(const uint8_t *, const int64_t *, int32_t, int32_t, int32_t, int32_t,
-                        const KParams &, int32_t *, void *, size_t, hipStream_t) {
-  return TSA_EINVAL;
+bool pencil_shape_supported(int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  return pencil_shape_ok(max_la, max_lb, max_lc);
+}
+
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, a),
+                                                                __builtin_bit_cast(s16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, b) +
+                                          __builtin_bit_cast(u16x2, c));
+}
+// per-half (a & b) != 0 -> 1 / 0
+__device__ __forceinline__ uint32_t pk_eq1(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(
+      uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a & b), (u16x2){1, 1}));
+}
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
+  return (mask & a) | (~mask & b);
+}
+// One LDS-DMA of 16 B per lane: LDS[m0 + lane*16] <- *gsrc (sc1: bypass L1).
+// Issued from inline asm so that hipcc does not treat it as an in-flight LDS
+// write and drain vmcnt(0) before every ds_read of the step loop; the
+// consumer waits for it with an explicit counted s_waitcnt vmcnt
+// (cdna_hip_programming.md 5.7: M0 must be set in the same statement).
+__device__ __forceinline__ void dma16(const void *gsrc, const void *lds_dst) {
+  unsigned keep;
+  const unsigned dst = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void *)lds_dst;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off sc1\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(dst))
+      : "memory");
+}
+__device__ __forceinline__ uint32_t ror1(uint32_t v) {  // lane l <- lane l-1, lane 0 <- lane 63
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xF, 0xF, false);
+}
+
+// Shift a packed per-position value one position up the helix (k <- k-1):
+// lanes >= 1 take lane-1's pair as is; lane 0 takes (pair i-1).hi and
+// (pair i).lo of lane 63; position 0 (lane 0, pair 0, lo) gets `inj`.
+template <int M>
+__device__ __forceinline__ void shift_pos(uint32_t (&v)[M], uint32_t sel, uint32_t mask0,
+                                          uint32_t inj) {
+  uint32_t r[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) r[i] = ror1(v[i]);
+#pragma unroll
+  for (int i = 0; i < M; ++i) v[i] = __builtin_amdgcn_perm(r[i], r[(i + M - 1) % M], sel);
+  v[0] = bfi(mask0, inj, v[0]);
+}
+
+template <int M, int NW>
+__global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restrict__ seqs,
+                                                         const int64_t *__restrict__ offs,
+                                                         int32_t n, int32_t P, int32_t R,
+                                                         int64_t ring_stride,
+                                                         uint8_t *__restrict__ ring_base,
+                                                         int32_t *__restrict__ scores,
+                                                         PencilArgs pa) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int PAIR_BYTES = 64 * REC_BYTES;              // one pair's record, 1 KiB
+  constexpr int SLOT_BYTES = M * PAIR_BYTES;
+  uint8_t *xr = smem;                                     // [NW-1][2][M][64][16]
+  uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT_BYTES;          // [PD][M][64][16]
+  uint8_t *sA = xr0 + PD * SLOT_BYTES;                    // [MAX_LA] one-hot symbols
+  uint8_t *sB = sA + MAX_LA;                              // [MAX_LB]
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t sel = lane == 0 ? 0x05040302u : 0x07060504u;
+  const uint32_t mask0 = lane == 0 ? 0x0000FFFFu : 0u;
+  constexpr int ZT = 128 * M;
+
+  for (int tri = blockIdx.x; tri < n; tri += gridDim.x) {
+    const int64_t o0 = offs[3 * (int64_t)tri], o1 = offs[3 * (int64_t)tri + 1];
+    const int64_t o2 = offs[3 * (int64_t)tri + 2], o3 = offs[3 * (int64_t)tri + 3];
+    const int32_t la = (int32_t)(o1 - o0), lb = (int32_t)(o2 - o1), lc = (int32_t)(o3 - o2);
+    uint8_t *ring = ring_base + (int64_t)blockIdx.x * ring_stride;
+
+    // ---- stage one-hot A (padded to P) and B; fill the ring with face records
+    for (int i = threadIdx.x; i < P; i += 64 * NW)
+      sA[i] = i < la ? (uint8_t)(1u << (seqs[o0 + i] & 3)) : 0;
+    for (int i = threadIdx.x; i < MAX_LB; i += 64 * NW)
+      sB[i] = i < lb ? (uint8_t)(1u << (seqs[o1 + i] & 3)) : 0;
+    {
+      const uint4 face = make_uint4(pa.f_single, pa.f_pair, pa.f_pair, 0u);
+      const int64_t n16 = (int64_t)R * M * 64;
+      for (int64_t i = threadIdx.x; i < n16; i += 64 * NW) ((uint4 *)ring)[i] = face;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // ---- per-position registers
+    uint32_t a[M], b[M], c[M];
+    uint32_t oIx[M], shIz[M], shIxz1[M], shIxz2[M], svIxy[M], svIyz[M], svM1[M], svM2[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const int k0 = lane + 128 * i, k1 = lane + 64 + 128 * i;
+      const uint32_t c0 = k0 < lc ? 1u << (seqs[o2 + k0] & 3) : 0u;
+      const uint32_t c1 = k1 < lc ? 1u << (seqs[o2 + k1] & 3) : 0u;
+      c[i] = c0 | (c1 << 16);
+      // symbols at step 0: position k is at u = -w-k (x index (u mod P))
+      const int x0 = ((-w - k0) % P + P) % P, x1 = ((-w - k1) % P + P) % P;
+      a[i] = (uint32_t)sA[x0] | ((uint32_t)sA[x1] << 16);
+      // only position 0 of wave 0 has started (u = 0, row 1); others are u < 0
+      b[i] = (i == 0 && w == 0 && lane == 0) ? (uint32_t)sB[0] : 0u;
+      oIx[i] = pa.f_single;
+      shIz[i] = pa.f_single;
+      shIxz1[i] = shIxz2[i] = pa.f_pair;
+      svIxy[i] = svIyz[i] = pa.f_pair;
+      svM1[i] = svM2[i] = 0;
+    }
+    // position-0 bookkeeping (wave-uniform): u0 = t - w
+    int32_t xpos0 = (P - (w % P)) % P;      // (t - w) mod P at t = 0
+    int32_t lap0 = w == 0 ? 0 : -1;         // floor((t - w) / P)
+    // final cell (la, lb, lc)
+    const int32_t lap_f = (lb - 1) / NW, w_f = (lb - 1) % NW, k_f = lc - 1;
+    const int32_t t_f = lap_f * P + (la - 1) + w_f + k_f;
+    const int32_t l_f = k_f & 63, i_f = k_f >> 7, h_f = (k_f >> 6) & 1;
+    const int32_t T = t_f + 1;
+
+    // wave 0: prime the LDS-DMA pipeline (ring row of step s = s - P + NW - 1)
+    const int32_t lag = P - (NW - 1);
+    if (w == 0) {
+#pragma unroll 1
+      for (int s = 0; s < PD; ++s) {
+        const int32_t row = ((s - lag) % R + R) % R;
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+          dma16(ring + ((int64_t)row * M + i) * PAIR_BYTES + lane * REC_BYTES,
+                xr0 + (s % PD) * SLOT_BYTES + i * PAIR_BYTES);
+      }
+    }
+    int32_t dma_row = ((PD - lag) % R + R) % R;  // ring row for step t + PD
+    int32_t st_row = 0;                          // ring row written at step t (last wave)
+
+#pragma unroll 1
+    for (int32_t t = 0; t < T; ++t) {
+      // ---- receive the wave-above record of step t-1
+      uint4 rec[M];
+      if (w == 0) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(M * (PD - 1)) : "memory");
+        const uint4 *src = (const uint4 *)__builtin_assume_aligned(
+            xr0 + (t % PD) * SLOT_BYTES + lane * REC_BYTES, 16);
+#pragma unroll
+        for (int i = 0; i < M; ++i) rec[i] = src[i * 64];
+      } else {
+        const uint4 *src = (const uint4 *)__builtin_assume_aligned(
+            xr + ((w - 1) * 2 + ((t - 1) & 1)) * SLOT_BYTES + lane * REC_BYTES, 16);
+#pragma unroll
+        for (int i = 0; i < M; ++i) rec[i] = src[i * 64];
+      }
+
+      // ---- inputs (messages into this cell)
+      uint32_t inIx[M], inIy[M], inIz[M], inIxy[M], inIyz[M], inIxz[M], inM[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        inIx[i] = oIx[i];
+        inIy[i] = rec[i].x;
+        inIz[i] = shIz[i];
+        inIxy[i] = svIxy[i];
+        inIyz[i] = svIyz[i];
+        inIxz[i] = shIxz2[i];
+        inM[i] = svM2[i];
+      }
+      // x == 1 at position k* = (t - w) mod P: its x-1 inputs are the x = 0 face
+      // (EN_i==1&&EN==0 gating, src/PE_1cyc.v:164-178,196-202,212-218)
+      if (xpos0 < ZT) {
+        const int ks = xpos0;
+        const uint32_t hm = (ks >> 6) & 1 ? 0xFFFF0000u : 0x0000FFFFu;
+        const uint32_t m1 = lane == (ks & 63) ? hm : 0u;
+        const int is = ks >> 7;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          if (i == is) {
+            inIx[i] = bfi(m1, pa.f_single, inIx[i]);
+            inIxy[i] = bfi(m1, pa.f_pair, inIxy[i]);
+            inIxz[i] = bfi(m1, pa.f_pair, inIxz[i]);
+            inM[i] = bfi(m1, 0u, inM[i]);
+          }
+        }
+      }
+
+      uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        // ---- scores (src/PE_1cyc.v:159-162) on one-hot symbols
+        const uint32_t eab = pk_eq1(a[i], b[i]);
+        const uint32_t eac = pk_eq1(a[i], c[i]);
+        const uint32_t ebc = pk_eq1(b[i], c[i]);
+        const uint32_t s2ab = pk_mad(eab, pa.dm, pa.mm);
+        const uint32_t s2ac = pk_mad(eac, pa.dm, pa.mm);
+        const uint32_t s2bc = pk_mad(ebc, pa.dm, pa.mm);
+        uint32_t s3;
+        if (pa.sop) s3 = pk_add(pk_add(s2ab, s2bc), s2ac);
+        else s3 = pk_mad(eab, pk_mad(ebc, pa.s3_d1, pa.s3_d0), pa.s3_ne);
+        // ---- states
+        const uint32_t sM = pk_add(inM[i], s3);
+        const uint32_t sX = inIx[i], sY = inIy[i], sZ = inIz[i];
+        const uint32_t sXY = pk_add(inIxy[i], s2ab);
+        const uint32_t sYZ = pk_add(inIyz[i], s2bc);
+        const uint32_t sXZ = pk_add(inIxz[i], s2ac);
+        // ---- messages: max_s(S[s] - P[T][s]), grouped by equal penalty
+        const uint32_t pYZ = pk_max(sY, sZ), pXZ = pk_max(sX, sZ), pXY = pk_max(sX, sY);
+        const uint32_t qXY_XZ = pk_max(sXY, sXZ), qXY_YZ = pk_max(sXY, sYZ), qYZ_XZ = pk_max(sYZ, sXZ);
+        const uint32_t A1 = pk_max(pYZ, qXY_XZ);  // Ix  <- {Iy,Iz,Ixy,Ixz} at GO+GE
+        const uint32_t A2 = pk_max(pXZ, qXY_YZ);  // Iy  <- {Ix,Iz,Ixy,Iyz}
+        const uint32_t A3 = pk_max(pXY, qYZ_XZ);  // Iz  <- {Ix,Iy,Iyz,Ixz}
+        const uint32_t B1 = pk_max(sM, sYZ);      // Ix  <- {M,Iyz} at 2GO
+        const uint32_t B2 = pk_max(sM, sXZ);      // Iy  <- {M,Ixz}
+        const uint32_t B3 = pk_max(sM, sXY);      // Iz  <- {M,Ixy}
+        const uint32_t C1 = pk_max(pXY, sXY);     // Ixy <- {Ix,Iy,Ixy} at GE
+        const uint32_t C2 = pk_max(pYZ, sYZ);     // Iyz <- {Iy,Iz,Iyz}
+        const uint32_t C3 = pk_max(pXZ, sXZ);     // Ixz <- {Ix,Iz,Ixz}
+        const uint32_t D1 = pk_max(B1, pk_max(sZ, sXZ));  // Ixy <- {M,Iz,Iyz,Ixz} at GO
+        const uint32_t D2 = pk_max(B2, pk_max(sX, sXY));  // Iyz <- {M,Ix,Ixy,Ixz}
+        const uint32_t D3 = pk_max(B3, pk_max(sY, sYZ));  // Ixz <- {M,Iy,Ixy,Iyz}
+        oBest[i] = pk_max(pk_max(A1, B1), sX);            // MAX7 of the states
+        nIx[i] = pk_max(pk_max(pk_sub(sX, pa.E2), pk_sub(A1, pa.OE)), pk_sub(B1, pa.O2));
+        oIy[i] = pk_max(pk_max(pk_sub(sY, pa.E2), pk_sub(A2, pa.OE)), pk_sub(B2, pa.O2));
+        oIz[i] = pk_max(pk_max(pk_sub(sZ, pa.E2), pk_sub(A3, pa.OE)), pk_sub(B3, pa.O2));
+        oIxy[i] = pk_max(pk_sub(C1, pa.E), pk_sub(D1, pa.O));
+        oIyz[i] = pk_max(pk_sub(C2, pa.E), pk_sub(D2, pa.O));
+        oIxz[i] = pk_max(pk_sub(C3, pa.E), pk_sub(D3, pa.O));
+      }
+
+      // ---- send this step's record to the wave below (or the ring)
+      if (w < NW - 1) {
+        uint4 *dst = (uint4 *)__builtin_assume_aligned(
+            xr + (w * 2 + (t & 1)) * SLOT_BYTES + lane * REC_BYTES, 16);
+#pragma unroll
+        for (int i = 0; i < M; ++i) dst[i * 64] = make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]);
+      } else {
+        uint8_t *dst = ring + (int64_t)st_row * SLOT_BYTES + lane * REC_BYTES;
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+          *(uint4 *)(dst + i * PAIR_BYTES) = make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]);
+      }
+
+      // ---- final cell (src/TriAlign_1cyc.v:141-142,342-345)
+      if (t == t_f && w == w_f) {
+        uint32_t v = oBest[0];
+#pragma unroll
+        for (int i = 1; i < M; ++i) if (i == i_f) v = oBest[i];
+        if (lane == l_f) scores[tri] = (int32_t)(int16_t)(h_f ? (v >> 16) : (v & 0xFFFF));
+      }
+
+      // ---- advance the systolic registers
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        oIx[i] = nIx[i];
+        shIxz2[i] = shIxz1[i];
+        shIxz1[i] = oIxz[i];
+        shIz[i] = oIz[i];
+        svIxy[i] = rec[i].y;
+        svIyz[i] = rec[i].z;
+        svM2[i] = svM1[i];
+        svM1[i] = rec[i].w;
+      }
+      shift_pos<M>(shIxz1, sel, mask0, pa.f_pair);   // z = 0 face for position 0
+      shift_pos<M>(shIz, sel, mask0, pa.f_single);
+      shift_pos<M>(svIyz, sel, mask0, pa.f_pair);
+      shift_pos<M>(svM1, sel, mask0, 0u);
+      // position 0 advances to u0 + 1
+      ++xpos0;
+      if (xpos0 == P) { xpos0 = 0; ++lap0; }
+      {
+        const uint32_t ainj = sA[xpos0];
+        const int32_t row0 = lap0 * NW + w;
+        const uint32_t binj = (lap0 >= 0 && row0 < lb) ? (uint32_t)sB[row0] : 0u;
+        shift_pos<M>(a, sel, mask0, ainj);
+        shift_pos<M>(b, sel, mask0, binj);
+      }
+
+      // ---- wave 0: fetch the record of step t + PD into the slot just consumed
+      if (w == 0) {
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+          dma16(ring + ((int64_t)dma_row * M + i) * PAIR_BYTES + lane * REC_BYTES,
+                xr0 + (t % PD) * SLOT_BYTES + i * PAIR_BYTES);
+        if (++dma_row == R) dma_row = 0;
+      }
+      if (w == NW - 1) {
+        if (++st_row == R) st_row = 0;
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(M * STORE_SLACK) : "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+}
+
+static PencilArgs make_args(const KParams &kp) {
+  auto pk = [](int32_t v) { return ((uint32_t)(uint16_t)(int16_t)v) * 0x00010001u; };
+  const int32_t GE = kp.pen[SIXY][SIX], GO = kp.pen[SIXY][SM];  // Ixy row: Ix = GE, M = GO
+  PencilArgs a;
+  a.E = pk(GE);
+  a.O = pk(GO);
+  a.E2 = pk(2 * GE);
+  a.OE = pk(GO + GE);
+  a.O2 = pk(2 * GO);
+  int32_t fs = -kp.pen[SIX][0], fp = -kp.pen[SIXY][0];
+  for (int s = 0; s < 7; ++s) {
+    fs = std::max(fs, -kp.pen[SIX][s]);
+    fp = std::max(fp, -kp.pen[SIXY][s]);
+  }
+  a.f_single = pk(fs);
+  a.f_pair = pk(fp);
+  a.dm = pk(kp.match - kp.mismatch);
+  a.mm = pk(kp.mismatch);
+  a.s3_d1 = pk(kp.s3_eq - kp.s3_ab);
+  a.s3_d0 = pk(kp.s3_ab - kp.s3_ne);
+  a.s3_ne = pk(kp.s3_ne);
+  a.sop = kp.s3_mode == TSA_S3_SOP;
+  return a;
+}
+
+template <int M>
+static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
+                    const PencilGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
+                    hipStream_t stream) {
+  constexpr int NW = PENCIL_NW;
+  const size_t lds = (size_t)(NW - 1) * 2 * M * 1024 + (size_t)PD * M * 1024 + MAX_LA + MAX_LB;
+  auto kfn = pencil_kernel<M, NW>;
+  if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return TSA_EDEVICE;
+  const int grid = n < 65535 ? n : 65535;
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * NW), lds, stream, d_seqs, d_offsets, n, g.P,
+                     g.R, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, pa);
+  return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
+}
+
+int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
+                        int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
+                        int32_t *d_scores, void *d_ws, size_t ws_bytes, hipStream_t stream) {
+  if (n <= 0) return TSA_OK;
+  if (!pencil_shape_ok(max_la, max_lb, max_lc)) return TSA_EINVAL;
+  const PencilGeom g = pencil_geom(max_la, max_lc);
+  const int32_t grid = n < 65535 ? n : 65535;
+  if (ws_bytes < (size_t)grid * (size_t)g.ring_bytes_per_triple) return TSA_ENOMEM;
+  const PencilArgs pa = make_args(kp);
+  if (g.M == 1) return launch_m<1>(d_seqs, d_offsets, n, g, d_scores, d_ws, pa, stream);
+  return launch_m<2>(d_seqs, d_offsets, n, g, d_scores, d_ws, pa, stream);
 }
 
 }  // namespace tsa

@@ -173,7 +173,8 @@ static bool pencil_exact(const tsa_params *p, int64_t la, int64_t lb, int64_t lc
   const int64_t lim_lo = p->score_bits ? -(1LL << (p->score_bits - 1)) : -32768;
   const int64_t lim_hi = p->score_bits ? (1LL << (p->score_bits - 1)) - 1 : 32767;
   return r.lo - PENCIL_MARGIN >= std::max<int64_t>(lim_lo, -32768) &&
-         r.hi + PENCIL_MARGIN <= std::min<int64_t>(lim_hi, 32767) && pencil_supported(p);
+         r.hi + PENCIL_MARGIN <= std::min<int64_t>(lim_hi, 32767) && pencil_supported(p) &&
+         pencil_shape_supported((int32_t)la, (int32_t)lb, (int32_t)lc);
 }
 
 static int choose_kernel(int32_t kernel, const tsa_params *p, int64_t la, int64_t lb, int64_t lc) {
