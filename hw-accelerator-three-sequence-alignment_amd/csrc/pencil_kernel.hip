@@ -102,14 +102,19 @@ __device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) {
 __device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
   return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
 }
+// v_pk_mad_u16 / v_pk_min_u16 written as asm: left to itself hipcc rewrites
+// min(x,1)*d+c into per-half compares and selects (6 ops instead of 2).
 __device__ __forceinline__ uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) {
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, b) +
-                                          __builtin_bit_cast(u16x2, c));
+  uint32_t r;
+  asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
 }
-// per-half (a & b) != 0 -> 1 / 0
-__device__ __forceinline__ uint32_t pk_eq1(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(
-      uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a & b), (u16x2){1, 1}));
+// per-half (a & b) != 0 -> 1 / 0 (one-hot symbols). `ones` = 0x00010001 in a
+// VGPR: a VOP3P inline constant would feed 0 to the high half.
+__device__ __forceinline__ uint32_t pk_eq1(uint32_t a, uint32_t b, uint32_t ones) {
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a & b), "v"(ones));
+  return r;
 }
 __device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
   return (mask & a) | (~mask & b);
@@ -133,7 +138,8 @@ __device__ __forceinline__ void dma16(const void *gsrc, const void *lds_dst) {
       : "memory");
 }
 __device__ __forceinline__ uint32_t ror1(uint32_t v) {  // lane l <- lane l-1, lane 0 <- lane 63
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xF, 0xF, false);
+  // mov_dpp (old = undef): wave_ror:1 reads a valid lane for every lane
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xF, 0xF, false);
 }
 
 // Shift a packed per-position value one position up the helix (k <- k-1):
@@ -170,6 +176,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t sel = lane == 0 ? 0x05040302u : 0x07060504u;
   const uint32_t mask0 = lane == 0 ? 0x0000FFFFu : 0u;
+  uint32_t ones = 0x00010001u;
+  asm volatile("" : "+v"(ones));  // keep it in a VGPR (VOP3P operand)
   constexpr int ZT = 128 * M;
 
   for (int tri = blockIdx.x; tri < n; tri += gridDim.x) {
@@ -286,9 +294,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         // ---- scores (src/PE_1cyc.v:159-162) on one-hot symbols
-        const uint32_t eab = pk_eq1(a[i], b[i]);
-        const uint32_t eac = pk_eq1(a[i], c[i]);
-        const uint32_t ebc = pk_eq1(b[i], c[i]);
+        const uint32_t eab = pk_eq1(a[i], b[i], ones);
+        const uint32_t eac = pk_eq1(a[i], c[i], ones);
+        const uint32_t ebc = pk_eq1(b[i], c[i], ones);
         const uint32_t s2ab = pk_mad(eab, pa.dm, pa.mm);
         const uint32_t s2ac = pk_mad(eac, pa.dm, pa.mm);
         const uint32_t s2bc = pk_mad(ebc, pa.dm, pa.mm);
@@ -332,10 +340,24 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll
         for (int i = 0; i < M; ++i) dst[i * 64] = make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]);
       } else {
-        uint8_t *dst = ring + (int64_t)st_row * SLOT_BYTES + lane * REC_BYTES;
+        // Positions that have not started (u = t - w - k < 0) must publish the
+        // y = 0 face: wave 0 reads this row as "row y0-1" during its lap 0.
+        if (t < ZT + NW) {
+          const int32_t lim = t - w;  // position k started iff k <= lim
 #pragma unroll
-        for (int i = 0; i < M; ++i)
-          *(uint4 *)(dst + i * PAIR_BYTES) = make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]);
+          for (int i = 0; i < M; ++i) {
+            const uint32_t m = ((lane + 128 * i > lim) ? 0x0000FFFFu : 0u) |
+                               ((lane + 64 + 128 * i > lim) ? 0xFFFF0000u : 0u);
+            oIy[i] = bfi(m, pa.f_single, oIy[i]);
+            oIxy[i] = bfi(m, pa.f_pair, oIxy[i]);
+            oIyz[i] = bfi(m, pa.f_pair, oIyz[i]);
+            oBest[i] = bfi(m, 0u, oBest[i]);
+          }
+        }
+        uint4 *dst = (uint4 *)__builtin_assume_aligned(
+            ring + (int64_t)st_row * SLOT_BYTES + lane * REC_BYTES, 16);
+#pragma unroll
+        for (int i = 0; i < M; ++i) dst[i * 64] = make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]);
       }
 
       // ---- final cell (src/TriAlign_1cyc.v:141-142,342-345)
