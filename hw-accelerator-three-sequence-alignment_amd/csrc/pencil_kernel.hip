@@ -32,6 +32,7 @@
 // Supported shapes: LC <= 128*M (M = 1 or 2), LA <= 4096, LB <= 4096.
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "pencil_kernel.h"
 
@@ -40,7 +41,9 @@ namespace tsa {
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
-constexpr int PENCIL_NW = 16;      // waves (= DP rows) per lap
+// waves (= DP rows) per lap: 16 (one 1024-thread WG per CU) or 8 (two WGs
+// per CU, so one computes while the other waits at its per-step barrier)
+constexpr int PENCIL_NW_DEFAULT = 16;
 constexpr int PD = 8;              // LDS-DMA prefetch distance of wave 0, steps
 constexpr int STORE_SLACK = 4;     // last wave keeps <= this many steps of stores in flight
 constexpr int PMIN = 48;           // >= PD + NW + STORE_SLACK + margin
@@ -160,7 +163,7 @@ template <int M, int NW>
 __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restrict__ seqs,
                                                          const int64_t *__restrict__ offs,
                                                          int32_t n, int32_t P, int32_t R,
-                                                         int64_t ring_stride,
+                                                         int32_t lds_a, int64_t ring_stride,
                                                          uint8_t *__restrict__ ring_base,
                                                          int32_t *__restrict__ scores,
                                                          PencilArgs pa) {
@@ -169,8 +172,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
   constexpr int SLOT_BYTES = M * PAIR_BYTES;
   uint8_t *xr = smem;                                     // [NW-1][2][M][64][16]
   uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT_BYTES;          // [PD][M][64][16]
-  uint8_t *sA = xr0 + PD * SLOT_BYTES;                    // [MAX_LA] one-hot symbols
-  uint8_t *sB = sA + MAX_LA;                              // [MAX_LB]
+  uint8_t *sA = xr0 + PD * SLOT_BYTES;                    // [lds_a >= P] one-hot A
+  uint8_t *sB = sA + lds_a;                               // [>= max LB] one-hot B
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -189,8 +192,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     // ---- stage one-hot A (padded to P) and B; fill the ring with face records
     for (int i = threadIdx.x; i < P; i += 64 * NW)
       sA[i] = i < la ? (uint8_t)(1u << (seqs[o0 + i] & 3)) : 0;
-    for (int i = threadIdx.x; i < MAX_LB; i += 64 * NW)
-      sB[i] = i < lb ? (uint8_t)(1u << (seqs[o1 + i] & 3)) : 0;
+    for (int i = threadIdx.x; i < lb; i += 64 * NW) sB[i] = (uint8_t)(1u << (seqs[o1 + i] & 3));
     {
       const uint4 face = make_uint4(pa.f_single, pa.f_pair, pa.f_pair, 0u);
       const int64_t n16 = (int64_t)R * M * 64;
@@ -439,19 +441,19 @@ static PencilArgs make_args(const KParams &kp) {
   return a;
 }
 
-template <int M>
+template <int M, int NW>
 static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
-                    const PencilGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
-                    hipStream_t stream) {
-  constexpr int NW = PENCIL_NW;
-  const size_t lds = (size_t)(NW - 1) * 2 * M * 1024 + (size_t)PD * M * 1024 + MAX_LA + MAX_LB;
+                    int32_t max_lb, const PencilGeom &g, int32_t *d_scores, void *d_ws,
+                    const PencilArgs &pa, hipStream_t stream) {
+  const int32_t lds_a = (g.P + 15) & ~15, lds_b = (max_lb + 15) & ~15;
+  const size_t lds = (size_t)(NW - 1) * 2 * M * 1024 + (size_t)PD * M * 1024 + lds_a + lds_b;
   auto kfn = pencil_kernel<M, NW>;
   if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return TSA_EDEVICE;
   const int grid = n < 65535 ? n : 65535;
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * NW), lds, stream, d_seqs, d_offsets, n, g.P,
-                     g.R, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, pa);
+                     g.R, lds_a, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, pa);
   return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
 }
 
@@ -464,8 +466,13 @@ int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t
   const int32_t grid = n < 65535 ? n : 65535;
   if (ws_bytes < (size_t)grid * (size_t)g.ring_bytes_per_triple) return TSA_ENOMEM;
   const PencilArgs pa = make_args(kp);
-  if (g.M == 1) return launch_m<1>(d_seqs, d_offsets, n, g, d_scores, d_ws, pa, stream);
-  return launch_m<2>(d_seqs, d_offsets, n, g, d_scores, d_ws, pa, stream);
+  int nw = PENCIL_NW_DEFAULT;
+  if (const char *e = getenv("TSA_PENCIL_NW")) nw = atoi(e) == 8 ? 8 : 16;  // tuning knob
+  if (g.M == 1)
+    return nw == 8 ? launch_m<1, 8>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_ws, pa, stream)
+                   : launch_m<1, 16>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_ws, pa, stream);
+  return nw == 8 ? launch_m<2, 8>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_ws, pa, stream)
+                 : launch_m<2, 16>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_ws, pa, stream);
 }
 
 }  // namespace tsa

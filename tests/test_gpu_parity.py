@@ -140,6 +140,15 @@ def test_pencil_shapes_vs_oracle(gpu, orc):
         assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (la, lb, lc)
 
 
+@pytest.mark.parametrize("nw", ["8", "16"])
+def test_pencil_waves_per_workgroup(gpu, orc, monkeypatch, nw):
+    monkeypatch.setenv("TSA_PENCIL_NW", nw)
+    rng = np.random.default_rng(int(nw))
+    for la, lb, lc in [(256, 40, 256), (100, 9, 130), (33, 70, 64), (300, 25, 255)]:
+        a, b, c = (rng.integers(0, 5, n).astype(np.uint8) for n in (la, lb, lc))
+        assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (nw, la, lb, lc)
+
+
 def test_pencil_ragged_batch(gpu, orc):
     rng = np.random.default_rng(77)
     triples = []

@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""A/B timing of kernel variants in ONE process, interleaved rounds (guide
+rule 24). Variants are environment knobs read by libtrialign at launch.
+  python tools/bench_variants.py --variants "TSA_PENCIL_NW=16" "TSA_PENCIL_NW=8" [--n 512 --L 256]
+Prints one JSON line per variant (median/min ms, GCUPS) to stdout."""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", nargs="+", required=True)
+    ap.add_argument("--n", type=int, default=512)
+    ap.add_argument("--L", type=int, default=256)
+    ap.add_argument("--kernel", default="pencil")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--check", action="store_true")
+    args = ap.parse_args()
+    import torch
+    import bench
+    tsa = bench.load_pkg()
+    import tsa_amd.synth as synth
+    L, n = args.L, args.n
+    seqs, offs = synth.batch(0, n, L)
+    d_seqs, d_offs = torch.from_numpy(seqs).cuda(), torch.from_numpy(offs).cuda()
+    d_scores = torch.zeros(n, dtype=torch.int32, device="cuda")
+    p = tsa.TsaParams.default()
+    ws = tsa.workspace_size(n, L, L, L, p, args.kernel)
+    d_ws = torch.empty(ws, dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream()
+    times = {v: [] for v in args.variants}
+    scores = {}
+
+    def run(v):
+        k, val = v.split("=", 1)
+        os.environ[k] = val
+        tsa.score_batch_async(d_seqs.data_ptr(), d_offs.data_ptr(), n, L, L, L, d_scores.data_ptr(),
+                              d_ws.data_ptr(), ws, st.cuda_stream, p, args.kernel)
+
+    for v in args.variants:  # warm-up
+        run(v)
+    torch.cuda.synchronize()
+    for _ in range(args.rounds):
+        for v in args.variants:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            run(v)
+            e1.record(st)
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1))
+            scores[v] = d_scores.cpu().numpy().copy()
+    ref = None
+    if args.check:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        idx = list(range(0, n, max(1, n // 8)))
+        trip = [synth.triple(i, L) for i in idx]
+        cs, co = tsa.pack_batch(trip)
+        ref = oracle.score_batch(cs, co, nthreads=8)
+    for v in args.variants:
+        med = statistics.median(times[v])
+        rec = {"variant": v, "n": n, "L": L, "median_ms": round(med, 4), "min_ms": round(min(times[v]), 4),
+               "gcups": round(n * L ** 3 / (med * 1e-3) / 1e9, 2)}
+        if ref is not None:
+            rec["parity_ok"] = bool((scores[v][idx] == ref).all())
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
