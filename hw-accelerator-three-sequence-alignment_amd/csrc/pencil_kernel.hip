@@ -33,6 +33,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "pencil_kernel.h"
 
@@ -85,8 +86,37 @@ static bool pencil_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc) {
          max_lc <= 256;
 }
 
+// Lap-parallel mode (pencil_lap_kernel) for small batches of tall cubes: every
+// lap of every triple gets its own resident workgroup.
+constexpr int LAP_NW = 16;
+constexpr int MAX_RESIDENT_WG = 256;  // one 1024-thread workgroup per CU
+struct LapGeom {
+  int32_t G, YR;
+  size_t yf_bytes, flag_bytes;
+};
+static LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  LapGeom g;
+  const int32_t M = pencil_pairs(max_lc);
+  g.G = (max_lb + LAP_NW - 1) / LAP_NW;
+  g.YR = max_la + max_lc + 2 * LAP_NW + PD + 8;
+  g.yf_bytes = (size_t)n * g.G * g.YR * M * 64 * REC_BYTES;
+  g.flag_bytes = (((size_t)n * g.G + 1) * sizeof(int32_t) + 255) & ~(size_t)255;
+  return g;
+}
+static bool use_lap_mode(int32_t n, int32_t max_lb) {
+  if (const char *e = getenv("TSA_PENCIL_MODE")) {
+    if (!strcmp(e, "helix")) return false;
+  }
+  const int32_t G = (max_lb + LAP_NW - 1) / LAP_NW;
+  return G >= 2 && (int64_t)n * G <= MAX_RESIDENT_WG;
+}
+
 size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
   if (!pencil_shape_ok(max_la, max_lb, max_lc)) return 0;
+  if (use_lap_mode(n, max_lb)) {
+    const LapGeom g = lap_geom(n, max_la, max_lb, max_lc);
+    return g.flag_bytes + g.yf_bytes;
+  }
   return (size_t)n * (size_t)pencil_geom(max_la, max_lc).ring_bytes_per_triple;
 }
 
@@ -157,6 +187,79 @@ __device__ __forceinline__ void shift_pos(uint32_t (&v)[M], uint32_t sel, uint32
 #pragma unroll
   for (int i = 0; i < M; ++i) v[i] = __builtin_amdgcn_perm(r[i], r[(i + M - 1) % M], sel);
   v[0] = bfi(mask0, inj, v[0]);
+}
+
+// The x == 1 position k* (if inside this lane span) takes the x = 0 face for
+// its x-1 inputs (EN_i==1&&EN==0 gating, src/PE_1cyc.v:164-178,196-202,212-218).
+template <int M>
+__device__ __forceinline__ void x1_substitute(int ks, int lane, const PencilArgs &pa,
+                                              uint32_t (&inIx)[M], uint32_t (&inIxy)[M],
+                                              uint32_t (&inIxz)[M], uint32_t (&inM)[M]) {
+  if (ks >= 0 && ks < 128 * M) {
+    const uint32_t hm = (ks >> 6) & 1 ? 0xFFFF0000u : 0x0000FFFFu;
+    const uint32_t m1 = lane == (ks & 63) ? hm : 0u;
+    const int is = ks >> 7;
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      if (i == is) {
+        inIx[i] = bfi(m1, pa.f_single, inIx[i]);
+        inIxy[i] = bfi(m1, pa.f_pair, inIxy[i]);
+        inIxz[i] = bfi(m1, pa.f_pair, inIxz[i]);
+        inM[i] = bfi(m1, 0u, inM[i]);
+      }
+    }
+  }
+}
+
+// One step of M packed cell pairs: scores (src/PE_1cyc.v:159-162) on one-hot
+// symbols, the 7 states, and the 7 outgoing messages max_s(S[s] - P[T][s])
+// (src/PE_1cyc.v:164-218) grouped by equal penalty; oBest = MAX7 of the states.
+template <int M>
+__device__ __forceinline__ void cell_messages(
+    const uint32_t (&a)[M], const uint32_t (&b)[M], const uint32_t (&c)[M], uint32_t ones,
+    const PencilArgs &pa, const uint32_t (&inIx)[M], const uint32_t (&inIy)[M],
+    const uint32_t (&inIz)[M], const uint32_t (&inIxy)[M], const uint32_t (&inIyz)[M],
+    const uint32_t (&inIxz)[M], const uint32_t (&inM)[M], uint32_t (&nIx)[M], uint32_t (&oIy)[M],
+    uint32_t (&oIz)[M], uint32_t (&oIxy)[M], uint32_t (&oIyz)[M], uint32_t (&oIxz)[M],
+    uint32_t (&oBest)[M]) {
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const uint32_t eab = pk_eq1(a[i], b[i], ones);
+    const uint32_t eac = pk_eq1(a[i], c[i], ones);
+    const uint32_t ebc = pk_eq1(b[i], c[i], ones);
+    const uint32_t s2ab = pk_mad(eab, pa.dm, pa.mm);
+    const uint32_t s2ac = pk_mad(eac, pa.dm, pa.mm);
+    const uint32_t s2bc = pk_mad(ebc, pa.dm, pa.mm);
+    uint32_t s3;
+    if (pa.sop) s3 = pk_add(pk_add(s2ab, s2bc), s2ac);
+    else s3 = pk_mad(eab, pk_mad(ebc, pa.s3_d1, pa.s3_d0), pa.s3_ne);
+    const uint32_t sM = pk_add(inM[i], s3);
+    const uint32_t sX = inIx[i], sY = inIy[i], sZ = inIz[i];
+    const uint32_t sXY = pk_add(inIxy[i], s2ab);
+    const uint32_t sYZ = pk_add(inIyz[i], s2bc);
+    const uint32_t sXZ = pk_add(inIxz[i], s2ac);
+    const uint32_t pYZ = pk_max(sY, sZ), pXZ = pk_max(sX, sZ), pXY = pk_max(sX, sY);
+    const uint32_t qXY_XZ = pk_max(sXY, sXZ), qXY_YZ = pk_max(sXY, sYZ), qYZ_XZ = pk_max(sYZ, sXZ);
+    const uint32_t A1 = pk_max(pYZ, qXY_XZ);  // Ix  <- {Iy,Iz,Ixy,Ixz} at GO+GE
+    const uint32_t A2 = pk_max(pXZ, qXY_YZ);  // Iy  <- {Ix,Iz,Ixy,Iyz}
+    const uint32_t A3 = pk_max(pXY, qYZ_XZ);  // Iz  <- {Ix,Iy,Iyz,Ixz}
+    const uint32_t B1 = pk_max(sM, sYZ);      // Ix  <- {M,Iyz} at 2GO
+    const uint32_t B2 = pk_max(sM, sXZ);      // Iy  <- {M,Ixz}
+    const uint32_t B3 = pk_max(sM, sXY);      // Iz  <- {M,Ixy}
+    const uint32_t C1 = pk_max(pXY, sXY);     // Ixy <- {Ix,Iy,Ixy} at GE
+    const uint32_t C2 = pk_max(pYZ, sYZ);     // Iyz <- {Iy,Iz,Iyz}
+    const uint32_t C3 = pk_max(pXZ, sXZ);     // Ixz <- {Ix,Iz,Ixz}
+    const uint32_t D1 = pk_max(B1, pk_max(sZ, sXZ));  // Ixy <- {M,Iz,Iyz,Ixz} at GO
+    const uint32_t D2 = pk_max(B2, pk_max(sX, sXY));  // Iyz <- {M,Ix,Ixy,Ixz}
+    const uint32_t D3 = pk_max(B3, pk_max(sY, sYZ));  // Ixz <- {M,Iy,Ixy,Iyz}
+    oBest[i] = pk_max(pk_max(A1, B1), sX);            // MAX7 of the states
+    nIx[i] = pk_max(pk_max(pk_sub(sX, pa.E2), pk_sub(A1, pa.OE)), pk_sub(B1, pa.O2));
+    oIy[i] = pk_max(pk_max(pk_sub(sY, pa.E2), pk_sub(A2, pa.OE)), pk_sub(B2, pa.O2));
+    oIz[i] = pk_max(pk_max(pk_sub(sZ, pa.E2), pk_sub(A3, pa.OE)), pk_sub(B3, pa.O2));
+    oIxy[i] = pk_max(pk_sub(C1, pa.E), pk_sub(D1, pa.O));
+    oIyz[i] = pk_max(pk_sub(C2, pa.E), pk_sub(D2, pa.O));
+    oIxz[i] = pk_max(pk_sub(C3, pa.E), pk_sub(D3, pa.O));
+  }
 }
 
 template <int M, int NW>
@@ -276,64 +379,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       }
       // x == 1 at position k* = (t - w) mod P: its x-1 inputs are the x = 0 face
       // (EN_i==1&&EN==0 gating, src/PE_1cyc.v:164-178,196-202,212-218)
-      if (xpos0 < ZT) {
-        const int ks = xpos0;
-        const uint32_t hm = (ks >> 6) & 1 ? 0xFFFF0000u : 0x0000FFFFu;
-        const uint32_t m1 = lane == (ks & 63) ? hm : 0u;
-        const int is = ks >> 7;
-#pragma unroll
-        for (int i = 0; i < M; ++i) {
-          if (i == is) {
-            inIx[i] = bfi(m1, pa.f_single, inIx[i]);
-            inIxy[i] = bfi(m1, pa.f_pair, inIxy[i]);
-            inIxz[i] = bfi(m1, pa.f_pair, inIxz[i]);
-            inM[i] = bfi(m1, 0u, inM[i]);
-          }
-        }
-      }
-
+      x1_substitute<M>(xpos0, lane, pa, inIx, inIxy, inIxz, inM);
       uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        // ---- scores (src/PE_1cyc.v:159-162) on one-hot symbols
-        const uint32_t eab = pk_eq1(a[i], b[i], ones);
-        const uint32_t eac = pk_eq1(a[i], c[i], ones);
-        const uint32_t ebc = pk_eq1(b[i], c[i], ones);
-        const uint32_t s2ab = pk_mad(eab, pa.dm, pa.mm);
-        const uint32_t s2ac = pk_mad(eac, pa.dm, pa.mm);
-        const uint32_t s2bc = pk_mad(ebc, pa.dm, pa.mm);
-        uint32_t s3;
-        if (pa.sop) s3 = pk_add(pk_add(s2ab, s2bc), s2ac);
-        else s3 = pk_mad(eab, pk_mad(ebc, pa.s3_d1, pa.s3_d0), pa.s3_ne);
-        // ---- states
-        const uint32_t sM = pk_add(inM[i], s3);
-        const uint32_t sX = inIx[i], sY = inIy[i], sZ = inIz[i];
-        const uint32_t sXY = pk_add(inIxy[i], s2ab);
-        const uint32_t sYZ = pk_add(inIyz[i], s2bc);
-        const uint32_t sXZ = pk_add(inIxz[i], s2ac);
-        // ---- messages: max_s(S[s] - P[T][s]), grouped by equal penalty
-        const uint32_t pYZ = pk_max(sY, sZ), pXZ = pk_max(sX, sZ), pXY = pk_max(sX, sY);
-        const uint32_t qXY_XZ = pk_max(sXY, sXZ), qXY_YZ = pk_max(sXY, sYZ), qYZ_XZ = pk_max(sYZ, sXZ);
-        const uint32_t A1 = pk_max(pYZ, qXY_XZ);  // Ix  <- {Iy,Iz,Ixy,Ixz} at GO+GE
-        const uint32_t A2 = pk_max(pXZ, qXY_YZ);  // Iy  <- {Ix,Iz,Ixy,Iyz}
-        const uint32_t A3 = pk_max(pXY, qYZ_XZ);  // Iz  <- {Ix,Iy,Iyz,Ixz}
-        const uint32_t B1 = pk_max(sM, sYZ);      // Ix  <- {M,Iyz} at 2GO
-        const uint32_t B2 = pk_max(sM, sXZ);      // Iy  <- {M,Ixz}
-        const uint32_t B3 = pk_max(sM, sXY);      // Iz  <- {M,Ixy}
-        const uint32_t C1 = pk_max(pXY, sXY);     // Ixy <- {Ix,Iy,Ixy} at GE
-        const uint32_t C2 = pk_max(pYZ, sYZ);     // Iyz <- {Iy,Iz,Iyz}
-        const uint32_t C3 = pk_max(pXZ, sXZ);     // Ixz <- {Ix,Iz,Ixz}
-        const uint32_t D1 = pk_max(B1, pk_max(sZ, sXZ));  // Ixy <- {M,Iz,Iyz,Ixz} at GO
-        const uint32_t D2 = pk_max(B2, pk_max(sX, sXY));  // Iyz <- {M,Ix,Ixy,Ixz}
-        const uint32_t D3 = pk_max(B3, pk_max(sY, sYZ));  // Ixz <- {M,Iy,Ixy,Iyz}
-        oBest[i] = pk_max(pk_max(A1, B1), sX);            // MAX7 of the states
-        nIx[i] = pk_max(pk_max(pk_sub(sX, pa.E2), pk_sub(A1, pa.OE)), pk_sub(B1, pa.O2));
-        oIy[i] = pk_max(pk_max(pk_sub(sY, pa.E2), pk_sub(A2, pa.OE)), pk_sub(B2, pa.O2));
-        oIz[i] = pk_max(pk_max(pk_sub(sZ, pa.E2), pk_sub(A3, pa.OE)), pk_sub(B3, pa.O2));
-        oIxy[i] = pk_max(pk_sub(C1, pa.E), pk_sub(D1, pa.O));
-        oIyz[i] = pk_max(pk_sub(C2, pa.E), pk_sub(D2, pa.O));
-        oIxz[i] = pk_max(pk_sub(C3, pa.E), pk_sub(D3, pa.O));
-      }
+      cell_messages<M>(a, b, c, ones, pa, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx, oIy, oIz,
+                       oIxy, oIyz, oIxz, oBest);
 
       // ---- send this step's record to the wave below (or the ring)
       if (w < NW - 1) {
@@ -416,6 +465,209 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
   }
 }
 
+// ---------------------------------------------------------------------------
+// Single-cube variant: one 16-row lap per workgroup, all laps of a triple in
+// flight at once (blockIdx.x = tri * G + L). Lap L's last wave hands its
+// per-step record rows down to lap L+1's wave 0 through global memory:
+//   producer: write-through (sc1) row stores; each step a counted vmcnt proves
+//             rows <= tau-STORE_SLACK complete, then one agent-scope flag store
+//             publishes that count (MI355X_MICROARCH.md "Valid forms", row 1);
+//   consumer: before LDS-DMA'ing (sc1) a row it has not yet seen published, it
+//             drains its own queue and polls the flag with agent-scope loads.
+// Every workgroup of the grid must be resident (host: n*G <= resident WGs), so
+// a spinning consumer never blocks its producer. Spins are bounded: on
+// timeout the kernel sets *err and carries on (scores then invalid).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store16_sc1(void *gptr, uint4 v) {
+  const u32x4 d = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(gptr), "v"(d) : "memory");
+}
+
+template <int M, int NW>
+__global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
+    const uint8_t *__restrict__ seqs, const int64_t *__restrict__ offs, int32_t G, int32_t YR,
+    uint8_t *__restrict__ yf_base, int32_t *__restrict__ flags, int32_t *__restrict__ err,
+    int32_t *__restrict__ scores, PencilArgs pa) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int PAIR_BYTES = 64 * REC_BYTES;
+  constexpr int SLOT_BYTES = M * PAIR_BYTES;
+  uint8_t *xr = smem;                             // [NW-1][2][M][64][16]
+  uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT_BYTES;  // [PD][M][64][16]
+  uint8_t *sA = xr0 + PD * SLOT_BYTES;            // one-hot A
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t sel = lane == 0 ? 0x05040302u : 0x07060504u;
+  const uint32_t mask0 = lane == 0 ? 0x0000FFFFu : 0u;
+  uint32_t ones = 0x00010001u;
+  asm volatile("" : "+v"(ones));
+
+  const int32_t tri = blockIdx.x / G, L = blockIdx.x % G;
+  const int64_t o0 = offs[3 * (int64_t)tri], o1 = offs[3 * (int64_t)tri + 1];
+  const int64_t o2 = offs[3 * (int64_t)tri + 2], o3 = offs[3 * (int64_t)tri + 3];
+  const int32_t la = (int32_t)(o1 - o0), lb = (int32_t)(o2 - o1), lc = (int32_t)(o3 - o2);
+  const int32_t nlap = (lb + NW - 1) / NW;
+  if (L >= nlap) return;  // whole workgroup
+  const int32_t T = la + (NW - 1) + (lc - 1);      // steps of this lap
+  uint8_t *yf_mine = yf_base + ((int64_t)tri * G + L) * YR * SLOT_BYTES;
+  const uint8_t *yf_prev = yf_mine - (int64_t)YR * SLOT_BYTES;
+  int32_t *flag_mine = flags + (int64_t)tri * G + L;
+  const int32_t *flag_prev = flag_mine - 1;
+
+  for (int i = threadIdx.x; i < la; i += 64 * NW) sA[i] = (uint8_t)(1u << (seqs[o0 + i] & 3));
+  __syncthreads();
+
+  const int32_t y = L * NW + w + 1;                 // this wave's DP row
+  const uint32_t bw = y <= lb ? (1u << (seqs[o1 + y - 1] & 3)) * 0x00010001u : 0u;
+  uint32_t a[M], b[M], c[M];
+  uint32_t oIx[M], shIz[M], shIxz1[M], shIxz2[M], svIxy[M], svIyz[M], svM1[M], svM2[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const int k0 = lane + 128 * i, k1 = lane + 64 + 128 * i;
+    const uint32_t c0 = k0 < lc ? 1u << (seqs[o2 + k0] & 3) : 0u;
+    const uint32_t c1 = k1 < lc ? 1u << (seqs[o2 + k1] & 3) : 0u;
+    c[i] = c0 | (c1 << 16);
+    b[i] = bw;  // one row per wave: B is constant
+    a[i] = (i == 0 && w == 0 && lane == 0) ? (uint32_t)sA[0] : 0u;  // only (x=1,k=0) started
+    oIx[i] = pa.f_single;
+    shIz[i] = pa.f_single;
+    shIxz1[i] = shIxz2[i] = pa.f_pair;
+    svIxy[i] = svIyz[i] = pa.f_pair;
+    svM1[i] = svM2[i] = 0;
+  }
+  const int32_t w_f = (lb - 1) % NW, k_f = lc - 1;
+  const bool final_lap = L == (lb - 1) / NW;
+  const int32_t t_f = (la - 1) + w_f + k_f;
+  const int32_t l_f = k_f & 63, i_f = k_f >> 7, h_f = (k_f >> 6) & 1;
+
+  // wave 0 of lap L>0: row r of yf_prev feeds step r - (NW-1); prime PD steps
+  int32_t seen = 0;  // rows of yf_prev known complete
+  auto ensure = [&](int32_t r) {  // r < T: row r must be published
+    if (r < seen || r >= T) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (uint32_t spin = 0;; ++spin) {
+      seen = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(flag_prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (r < seen) break;
+      if (spin > (1u << 22)) {
+        if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        seen = T;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  if (w == 0 && L > 0) {
+    for (int s2 = 0; s2 < PD; ++s2) {
+      const int32_t r = s2 + NW - 1;
+      ensure(r);
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+        dma16(yf_prev + ((int64_t)r * M + i) * PAIR_BYTES + lane * REC_BYTES,
+              xr0 + (s2 % PD) * SLOT_BYTES + i * PAIR_BYTES);
+    }
+  }
+  const uint4 face = make_uint4(pa.f_single, pa.f_pair, pa.f_pair, 0u);
+
+#pragma unroll 1
+  for (int32_t t = 0; t < T; ++t) {
+    uint4 rec[M];
+    if (w == 0) {
+      if (L == 0) {
+#pragma unroll
+        for (int i = 0; i < M; ++i) rec[i] = face;  // y = 0 face
+      } else {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(M * (PD - 1)) : "memory");
+        const uint4 *src = (const uint4 *)__builtin_assume_aligned(
+            xr0 + (t % PD) * SLOT_BYTES + lane * REC_BYTES, 16);
+#pragma unroll
+        for (int i = 0; i < M; ++i) rec[i] = src[i * 64];
+      }
+    } else {
+      const uint4 *src = (const uint4 *)__builtin_assume_aligned(
+          xr + ((w - 1) * 2 + ((t - 1) & 1)) * SLOT_BYTES + lane * REC_BYTES, 16);
+#pragma unroll
+      for (int i = 0; i < M; ++i) rec[i] = src[i * 64];
+    }
+    uint32_t inIx[M], inIy[M], inIz[M], inIxy[M], inIyz[M], inIxz[M], inM[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      inIx[i] = oIx[i];
+      inIy[i] = rec[i].x;
+      inIz[i] = shIz[i];
+      inIxy[i] = svIxy[i];
+      inIyz[i] = svIyz[i];
+      inIxz[i] = shIxz2[i];
+      inM[i] = svM2[i];
+    }
+    x1_substitute<M>(t - w, lane, pa, inIx, inIxy, inIxz, inM);
+    uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
+    cell_messages<M>(a, b, c, ones, pa, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx, oIy, oIz,
+                     oIxy, oIyz, oIxz, oBest);
+
+    if (w < NW - 1) {
+      uint4 *dst = (uint4 *)__builtin_assume_aligned(
+          xr + (w * 2 + (t & 1)) * SLOT_BYTES + lane * REC_BYTES, 16);
+#pragma unroll
+      for (int i = 0; i < M; ++i) dst[i * 64] = make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+        store16_sc1(yf_mine + ((int64_t)t * M + i) * PAIR_BYTES + lane * REC_BYTES,
+                    make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
+    }
+    if (final_lap && t == t_f && w == w_f) {
+      uint32_t v = oBest[0];
+#pragma unroll
+      for (int i = 1; i < M; ++i) if (i == i_f) v = oBest[i];
+      if (lane == l_f) scores[tri] = (int32_t)(int16_t)(h_f ? (v >> 16) : (v & 0xFFFF));
+    }
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      oIx[i] = nIx[i];
+      shIxz2[i] = shIxz1[i];
+      shIxz1[i] = oIxz[i];
+      shIz[i] = oIz[i];
+      svIxy[i] = rec[i].y;
+      svIyz[i] = rec[i].z;
+      svM2[i] = svM1[i];
+      svM1[i] = rec[i].w;
+    }
+    shift_pos<M>(shIxz1, sel, mask0, pa.f_pair);
+    shift_pos<M>(shIz, sel, mask0, pa.f_single);
+    shift_pos<M>(svIyz, sel, mask0, pa.f_pair);
+    shift_pos<M>(svM1, sel, mask0, 0u);
+    {
+      const int32_t xi = t + 1 - w;  // position 0's x-1 at step t+1
+      const uint32_t ainj = (xi >= 0 && xi < la) ? (uint32_t)sA[xi] : 0u;
+      shift_pos<M>(a, sel, mask0, ainj);
+    }
+    if (w == 0 && L > 0) {
+      const int32_t r = t + PD + NW - 1;  // row for step t + PD
+      ensure(r);
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+        dma16(yf_prev + ((int64_t)r * M + i) * PAIR_BYTES + lane * REC_BYTES,
+              xr0 + (t % PD) * SLOT_BYTES + i * PAIR_BYTES);
+    }
+    if (w == NW - 1) {
+      // rows <= t - STORE_SLACK complete (M stores + 1 flag store per step)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STORE_SLACK * (M + 1)) : "memory");
+      // exactly M + 1 vector-memory ops per step keep that count exact
+      if (lane == 0)
+        __hip_atomic_store(flag_mine, t >= STORE_SLACK ? t - STORE_SLACK + 1 : 0,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  if (w == NW - 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(flag_mine, T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+
 static PencilArgs make_args(const KParams &kp) {
   auto pk = [](int32_t v) { return ((uint32_t)(uint16_t)(int16_t)v) * 0x00010001u; };
   const int32_t GE = kp.pen[SIXY][SIX], GO = kp.pen[SIXY][SM];  // Ixy row: Ix = GE, M = GO
@@ -457,11 +709,37 @@ static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
   return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
 }
 
+template <int M>
+static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, int32_t max_la,
+                      const LapGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
+                      hipStream_t stream) {
+  constexpr int NW = LAP_NW;
+  const size_t lds = (size_t)(NW - 1) * 2 * M * 1024 + (size_t)PD * M * 1024 + ((max_la + 15) & ~15);
+  auto kfn = pencil_lap_kernel<M, NW>;
+  if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)lds) != hipSuccess)
+    return TSA_EDEVICE;
+  int32_t *flags = (int32_t *)d_ws;           // [n*G] progress + [1] error word
+  if (hipMemsetAsync(flags, 0, g.flag_bytes, stream) != hipSuccess) return TSA_EDEVICE;
+  uint8_t *yf = (uint8_t *)d_ws + g.flag_bytes;
+  hipLaunchKernelGGL(kfn, dim3(n * g.G), dim3(64 * NW), lds, stream, d_seqs, d_offsets, g.G, g.YR,
+                     yf, flags, flags + (size_t)n * g.G, d_scores, pa);
+  return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
+}
+
 int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                         int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
                         int32_t *d_scores, void *d_ws, size_t ws_bytes, hipStream_t stream) {
   if (n <= 0) return TSA_OK;
   if (!pencil_shape_ok(max_la, max_lb, max_lc)) return TSA_EINVAL;
+  if (use_lap_mode(n, max_lb)) {
+    const LapGeom lg = lap_geom(n, max_la, max_lb, max_lc);
+    if (ws_bytes < lg.flag_bytes + lg.yf_bytes) return TSA_ENOMEM;
+    const PencilArgs pa = make_args(kp);
+    if (pencil_pairs(max_lc) == 1)
+      return launch_lap<1>(d_seqs, d_offsets, n, max_la, lg, d_scores, d_ws, pa, stream);
+    return launch_lap<2>(d_seqs, d_offsets, n, max_la, lg, d_scores, d_ws, pa, stream);
+  }
   const PencilGeom g = pencil_geom(max_la, max_lc);
   const int32_t grid = n < 65535 ? n : 65535;
   if (ws_bytes < (size_t)grid * (size_t)g.ring_bytes_per_triple) return TSA_ENOMEM;

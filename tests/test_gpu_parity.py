@@ -149,6 +149,29 @@ def test_pencil_waves_per_workgroup(gpu, orc, monkeypatch, nw):
         assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (nw, la, lb, lc)
 
 
+@pytest.mark.parametrize("mode", ["helix", "lap"])
+def test_pencil_single_cube_modes(gpu, orc, synth, monkeypatch, mode):
+    # "lap": one 16-row lap per workgroup, laps chained through global memory
+    # with progress flags; "helix": one workgroup walks all laps
+    if mode == "helix":
+        monkeypatch.setenv("TSA_PENCIL_MODE", "helix")
+    rng = np.random.default_rng(5 if mode == "helix" else 6)
+    for la, lb, lc in [(256, 256, 256), (64, 64, 64), (200, 17, 129), (31, 250, 100), (1, 40, 1),
+                       (500, 33, 256)]:
+        a, b, c = (rng.integers(0, 4, n).astype(np.uint8) for n in (la, lb, lc))
+        assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (mode, la, lb, lc)
+
+
+def test_pencil_lap_mode_small_batch(gpu, orc):
+    # several triples in lap mode at once (n * laps <= resident workgroups)
+    rng = np.random.default_rng(9)
+    triples = [tuple(rng.integers(0, 4, n).astype(np.uint8) for n in (int(rng.integers(1, 260)), int(rng.integers(17, 120)), int(rng.integers(1, 257))))
+               for _ in range(12)]
+    got = gpu.score_batch(triples)
+    seqs, offs = gpu.pack_batch(triples)
+    assert np.array_equal(got, orc.score_batch(seqs, offs, nthreads=8))
+
+
 def test_pencil_ragged_batch(gpu, orc):
     rng = np.random.default_rng(77)
     triples = []
