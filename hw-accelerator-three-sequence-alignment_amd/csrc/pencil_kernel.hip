@@ -46,6 +46,7 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 // per CU, so one computes while the other waits at its per-step barrier)
 constexpr int PENCIL_NW_DEFAULT = 16;
 constexpr int PD = 8;              // LDS-DMA prefetch distance of wave 0, steps
+constexpr int LPD = 4;             // prefetch distance of the lap kernel (cross-CU hand-off)
 constexpr int STORE_SLACK = 4;     // last wave keeps <= this many steps of stores in flight
 constexpr int PMIN = 48;           // >= PD + NW + STORE_SLACK + margin
 constexpr int MAX_LA = 4096, MAX_LB = 4096;
@@ -165,6 +166,20 @@ __device__ __forceinline__ void dma16(const void *gsrc, const void *lds_dst) {
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
       "global_load_lds_dwordx4 %1, off sc1\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(dst))
+      : "memory");
+}
+// 4-byte LDS-DMA from lane 0 only (the caller guards with lane == 0).
+__device__ __forceinline__ void dma4(const void *gsrc, const void *lds_dst) {
+  unsigned keep;
+  const unsigned dst = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void *)lds_dst;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, off sc1\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(dst))
@@ -492,8 +507,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
   constexpr int PAIR_BYTES = 64 * REC_BYTES;
   constexpr int SLOT_BYTES = M * PAIR_BYTES;
   uint8_t *xr = smem;                             // [NW-1][2][M][64][16]
-  uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT_BYTES;  // [PD][M][64][16]
-  uint8_t *sA = xr0 + PD * SLOT_BYTES;            // one-hot A
+  uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT_BYTES;  // [LPD][M][64][16]
+  int32_t *fslot = (int32_t *)(xr0 + LPD * SLOT_BYTES);  // [LPD] prefetched producer flags
+  uint8_t *sA = (uint8_t *)(fslot + LPD);          // one-hot A
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -540,7 +556,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
   const int32_t t_f = (la - 1) + w_f + k_f;
   const int32_t l_f = k_f & 63, i_f = k_f >> 7, h_f = (k_f >> 6) & 1;
 
-  // wave 0 of lap L>0: row r of yf_prev feeds step r - (NW-1); prime PD steps
+  // wave 0 of lap L>0: row r of yf_prev feeds step r - (NW-1); prime LPD steps
   int32_t seen = 0;  // rows of yf_prev known complete
   auto ensure = [&](int32_t r) {  // r < T: row r must be published
     if (r < seen || r >= T) return;
@@ -558,13 +574,14 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     }
   };
   if (w == 0 && L > 0) {
-    for (int s2 = 0; s2 < PD; ++s2) {
+    for (int s2 = 0; s2 < LPD; ++s2) {
       const int32_t r = s2 + NW - 1;
       ensure(r);
 #pragma unroll
       for (int i = 0; i < M; ++i)
         dma16(yf_prev + ((int64_t)r * M + i) * PAIR_BYTES + lane * REC_BYTES,
-              xr0 + (s2 % PD) * SLOT_BYTES + i * PAIR_BYTES);
+              xr0 + (s2 % LPD) * SLOT_BYTES + i * PAIR_BYTES);
+      if (lane == 0) dma4(flag_prev, fslot + (s2 % LPD));
     }
   }
   const uint4 face = make_uint4(pa.f_single, pa.f_pair, pa.f_pair, 0u);
@@ -577,11 +594,14 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
 #pragma unroll
         for (int i = 0; i < M; ++i) rec[i] = face;  // y = 0 face
       } else {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(M * (PD - 1)) : "memory");
+        // rows + flag of step t were DMA'd LPD steps ago: M+1 ops per step
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((M + 1) * (LPD - 1)) : "memory");
         const uint4 *src = (const uint4 *)__builtin_assume_aligned(
-            xr0 + (t % PD) * SLOT_BYTES + lane * REC_BYTES, 16);
+            xr0 + (t % LPD) * SLOT_BYTES + lane * REC_BYTES, 16);
 #pragma unroll
         for (int i = 0; i < M; ++i) rec[i] = src[i * 64];
+        // producer progress as of ~LPD steps ago, free of any round trip
+        seen = max(seen, __builtin_amdgcn_readfirstlane(fslot[t % LPD]));
       }
     } else {
       const uint4 *src = (const uint4 *)__builtin_assume_aligned(
@@ -643,12 +663,13 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
       shift_pos<M>(a, sel, mask0, ainj);
     }
     if (w == 0 && L > 0) {
-      const int32_t r = t + PD + NW - 1;  // row for step t + PD
-      ensure(r);
+      const int32_t r = t + LPD + NW - 1;  // row for step t + LPD
+      ensure(r);  // usually satisfied by the prefetched flag: no round trip
 #pragma unroll
       for (int i = 0; i < M; ++i)
         dma16(yf_prev + ((int64_t)r * M + i) * PAIR_BYTES + lane * REC_BYTES,
-              xr0 + (t % PD) * SLOT_BYTES + i * PAIR_BYTES);
+              xr0 + (t % LPD) * SLOT_BYTES + i * PAIR_BYTES);
+      if (lane == 0) dma4(flag_prev, fslot + (t % LPD));
     }
     if (w == NW - 1) {
       // rows <= t - STORE_SLACK complete (M stores + 1 flag store per step)
@@ -714,7 +735,8 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
                       const LapGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
                       hipStream_t stream) {
   constexpr int NW = LAP_NW;
-  const size_t lds = (size_t)(NW - 1) * 2 * M * 1024 + (size_t)PD * M * 1024 + ((max_la + 15) & ~15);
+  const size_t lds = (size_t)(NW - 1) * 2 * M * 1024 + (size_t)LPD * M * 1024 + LPD * 4 +
+                     ((max_la + 15) & ~15);
   auto kfn = pencil_lap_kernel<M, NW>;
   if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
