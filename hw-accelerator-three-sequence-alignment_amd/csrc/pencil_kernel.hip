@@ -89,17 +89,28 @@ static bool pencil_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc) {
 
 // Lap-parallel mode (pencil_lap_kernel) for small batches of tall cubes: every
 // lap of every triple gets its own resident workgroup.
-constexpr int LAP_NW = 16;
-constexpr int MAX_RESIDENT_WG = 256;  // one 1024-thread workgroup per CU
+// Rows per lap (waves per workgroup) of the lap kernel: fewer rows = shorter
+// steps but more laps, each adding a hand-off lag. Tuning knob TSA_LAP_NW.
+constexpr int LAP_NW_DEFAULT = 16;
+static int lap_nw() {
+  if (const char *e = getenv("TSA_LAP_NW")) {
+    const int v = atoi(e);
+    if (v == 4 || v == 8 || v == 16) return v;
+  }
+  return LAP_NW_DEFAULT;
+}
+// workgroups guaranteed co-resident: one per CU for 16 waves, two for 8, four for 4
+static int max_resident_wg(int nw) { return 256 * (16 / nw); }
 struct LapGeom {
-  int32_t G, YR;
+  int32_t NW, G, YR;
   size_t yf_bytes, flag_bytes;
 };
 static LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
   LapGeom g;
   const int32_t M = pencil_pairs(max_lc);
-  g.G = (max_lb + LAP_NW - 1) / LAP_NW;
-  g.YR = max_la + max_lc + 2 * LAP_NW + PD + 8;
+  g.NW = lap_nw();
+  g.G = (max_lb + g.NW - 1) / g.NW;
+  g.YR = max_la + max_lc + 2 * g.NW + PD + 8;
   g.yf_bytes = (size_t)n * g.G * g.YR * M * 64 * REC_BYTES;
   g.flag_bytes = (((size_t)n * g.G + 1) * sizeof(int32_t) + 255) & ~(size_t)255;
   return g;
@@ -108,8 +119,9 @@ static bool use_lap_mode(int32_t n, int32_t max_lb) {
   if (const char *e = getenv("TSA_PENCIL_MODE")) {
     if (!strcmp(e, "helix")) return false;
   }
-  const int32_t G = (max_lb + LAP_NW - 1) / LAP_NW;
-  return G >= 2 && (int64_t)n * G <= MAX_RESIDENT_WG;
+  const int nw = lap_nw();
+  const int32_t G = (max_lb + nw - 1) / nw;
+  return G >= 2 && (int64_t)n * G <= max_resident_wg(nw);
 }
 
 size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
@@ -184,6 +196,21 @@ __device__ __forceinline__ void dma4(const void *gsrc, const void *lds_dst) {
       : "=&s"(keep)
       : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(dst))
       : "memory");
+}
+// 16-byte LDS record read as one ds_read_b128 (lane-contiguous, conflict
+// free). Through a generic pointer hipcc splits it into two ds_read2_b32
+// with a 16 B lane stride, a 4-way bank conflict (SQ_LDS_BANK_CONFLICT).
+typedef unsigned u32x4_lds __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 lds_read16(const uint8_t *p) {
+  const __attribute__((address_space(3))) u32x4_lds *q =
+      (const __attribute__((address_space(3))) u32x4_lds *)(const __attribute__((address_space(3))) void *)p;
+  const u32x4_lds v = *q;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void lds_write16(uint8_t *p, uint4 v) {
+  __attribute__((address_space(3))) u32x4_lds *q =
+      (__attribute__((address_space(3))) u32x4_lds *)(__attribute__((address_space(3))) void *)p;
+  *q = (u32x4_lds){v.x, v.y, v.z, v.w};
 }
 __device__ __forceinline__ uint32_t ror1(uint32_t v) {  // lane l <- lane l-1, lane 0 <- lane 63
   // mov_dpp (old = undef): wave_ror:1 reads a valid lane for every lane
@@ -369,15 +396,13 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       uint4 rec[M];
       if (w == 0) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(M * (PD - 1)) : "memory");
-        const uint4 *src = (const uint4 *)__builtin_assume_aligned(
-            xr0 + (t % PD) * SLOT_BYTES + lane * REC_BYTES, 16);
+        const uint8_t *src = xr0 + (t % PD) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
-        for (int i = 0; i < M; ++i) rec[i] = src[i * 64];
+        for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
       } else {
-        const uint4 *src = (const uint4 *)__builtin_assume_aligned(
-            xr + ((w - 1) * 2 + ((t - 1) & 1)) * SLOT_BYTES + lane * REC_BYTES, 16);
+        const uint8_t *src = xr + ((w - 1) * 2 + ((t - 1) & 1)) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
-        for (int i = 0; i < M; ++i) rec[i] = src[i * 64];
+        for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
       }
 
       // ---- inputs (messages into this cell)
@@ -401,10 +426,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 
       // ---- send this step's record to the wave below (or the ring)
       if (w < NW - 1) {
-        uint4 *dst = (uint4 *)__builtin_assume_aligned(
-            xr + (w * 2 + (t & 1)) * SLOT_BYTES + lane * REC_BYTES, 16);
+        uint8_t *dst = xr + (w * 2 + (t & 1)) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
-        for (int i = 0; i < M; ++i) dst[i * 64] = make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]);
+        for (int i = 0; i < M; ++i)
+          lds_write16(dst + i * PAIR_BYTES, make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
       } else {
         // Positions that have not started (u = t - w - k < 0) must publish the
         // y = 0 face: wave 0 reads this row as "row y0-1" during its lap 0.
@@ -596,18 +621,16 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
       } else {
         // rows + flag of step t were DMA'd LPD steps ago: M+1 ops per step
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"((M + 1) * (LPD - 1)) : "memory");
-        const uint4 *src = (const uint4 *)__builtin_assume_aligned(
-            xr0 + (t % LPD) * SLOT_BYTES + lane * REC_BYTES, 16);
+        const uint8_t *src = xr0 + (t % LPD) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
-        for (int i = 0; i < M; ++i) rec[i] = src[i * 64];
+        for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
         // producer progress as of ~LPD steps ago, free of any round trip
         seen = max(seen, __builtin_amdgcn_readfirstlane(fslot[t % LPD]));
       }
     } else {
-      const uint4 *src = (const uint4 *)__builtin_assume_aligned(
-          xr + ((w - 1) * 2 + ((t - 1) & 1)) * SLOT_BYTES + lane * REC_BYTES, 16);
+      const uint8_t *src = xr + ((w - 1) * 2 + ((t - 1) & 1)) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
-      for (int i = 0; i < M; ++i) rec[i] = src[i * 64];
+      for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
     }
     uint32_t inIx[M], inIy[M], inIz[M], inIxy[M], inIyz[M], inIxz[M], inM[M];
 #pragma unroll
@@ -626,10 +649,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
                      oIxy, oIyz, oIxz, oBest);
 
     if (w < NW - 1) {
-      uint4 *dst = (uint4 *)__builtin_assume_aligned(
-          xr + (w * 2 + (t & 1)) * SLOT_BYTES + lane * REC_BYTES, 16);
+      uint8_t *dst = xr + (w * 2 + (t & 1)) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
-      for (int i = 0; i < M; ++i) dst[i * 64] = make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]);
+      for (int i = 0; i < M; ++i)
+        lds_write16(dst + i * PAIR_BYTES, make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
     } else {
 #pragma unroll
       for (int i = 0; i < M; ++i)
@@ -730,11 +753,10 @@ static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
   return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
 }
 
-template <int M>
+template <int M, int NW>
 static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, int32_t max_la,
                       const LapGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
                       hipStream_t stream) {
-  constexpr int NW = LAP_NW;
   const size_t lds = (size_t)(NW - 1) * 2 * M * 1024 + (size_t)LPD * M * 1024 + LPD * 4 +
                      ((max_la + 15) & ~15);
   auto kfn = pencil_lap_kernel<M, NW>;
@@ -758,9 +780,11 @@ int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t
     const LapGeom lg = lap_geom(n, max_la, max_lb, max_lc);
     if (ws_bytes < lg.flag_bytes + lg.yf_bytes) return TSA_ENOMEM;
     const PencilArgs pa = make_args(kp);
+#define TSA_LAP(MM, NN) launch_lap<MM, NN>(d_seqs, d_offsets, n, max_la, lg, d_scores, d_ws, pa, stream)
     if (pencil_pairs(max_lc) == 1)
-      return launch_lap<1>(d_seqs, d_offsets, n, max_la, lg, d_scores, d_ws, pa, stream);
-    return launch_lap<2>(d_seqs, d_offsets, n, max_la, lg, d_scores, d_ws, pa, stream);
+      return lg.NW == 4 ? TSA_LAP(1, 4) : lg.NW == 8 ? TSA_LAP(1, 8) : TSA_LAP(1, 16);
+    return lg.NW == 4 ? TSA_LAP(2, 4) : lg.NW == 8 ? TSA_LAP(2, 8) : TSA_LAP(2, 16);
+#undef TSA_LAP
   }
   const PencilGeom g = pencil_geom(max_la, max_lc);
   const int32_t grid = n < 65535 ? n : 65535;

@@ -1,0 +1,15 @@
+#!/bin/bash
+# SQ counters of the pencil batch launch (two passes, 8 SQ counters each).
+set -o pipefail
+R="$GRAFT_REPO_ROOT"; TAG=${TAG:-sq}
+cd /tmp && export TMPDIR=/tmp
+OUT="$R/gpurun_out/pmc_${TAG}"; mkdir -p "$OUT"
+i=0
+for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SALU SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace -d "$OUT/p$i" -o run --output-format csv \
+    -- python3 "$R/tools/bench_variants.py" --n ${N:-512} --rounds 1 --variants ${VARIANTS:-TSA_PENCIL_NW=16} \
+    > "$OUT/p$i.json" 2> "$OUT/p$i.err"
+  rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/p$i.err"; exit $rc; }
+done

@@ -162,6 +162,15 @@ def test_pencil_single_cube_modes(gpu, orc, synth, monkeypatch, mode):
         assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (mode, la, lb, lc)
 
 
+@pytest.mark.parametrize("nw", ["4", "8"])
+def test_pencil_lap_rows_per_lap(gpu, orc, synth, monkeypatch, nw):
+    monkeypatch.setenv("TSA_LAP_NW", nw)
+    rng = np.random.default_rng(40 + int(nw))
+    for la, lb, lc in [(256, 256, 256), (100, 37, 200), (17, 90, 5)]:
+        a, b, c = (rng.integers(0, 4, n).astype(np.uint8) for n in (la, lb, lc))
+        assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (nw, la, lb, lc)
+
+
 def test_pencil_lap_mode_small_batch(gpu, orc):
     # several triples in lap mode at once (n * laps <= resident workgroups)
     rng = np.random.default_rng(9)
