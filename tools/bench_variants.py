@@ -31,7 +31,16 @@ def main():
     d_seqs, d_offs = torch.from_numpy(seqs).cuda(), torch.from_numpy(offs).cuda()
     d_scores = torch.zeros(n, dtype=torch.int32, device="cuda")
     p = tsa.TsaParams.default()
-    ws = tsa.workspace_size(n, L, L, L, p, args.kernel)
+    ws = 0
+    for v in args.variants:  # workspace depends on the knobs: take the max
+        k, val = v.split("=", 1)
+        old = os.environ.get(k)
+        os.environ[k] = val
+        ws = max(ws, tsa.workspace_size(n, L, L, L, p, args.kernel))
+        if old is None:
+            del os.environ[k]
+        else:
+            os.environ[k] = old
     d_ws = torch.empty(ws, dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream()
     times = {v: [] for v in args.variants}
