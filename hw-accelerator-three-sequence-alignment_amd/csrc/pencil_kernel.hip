@@ -308,7 +308,8 @@ template <int M, int NW>
 __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restrict__ seqs,
                                                          const int64_t *__restrict__ offs,
                                                          int32_t n, int32_t P, int32_t R,
-                                                         int32_t lds_a, int64_t ring_stride,
+                                                         int32_t lds_a, int32_t stagger,
+                                                         int64_t ring_stride,
                                                          uint8_t *__restrict__ ring_base,
                                                          int32_t *__restrict__ scores,
                                                          PencilArgs pa) {
@@ -390,8 +391,19 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     int32_t dma_row = ((PD - lag) % R + R) % R;  // ring row for step t + PD
     int32_t st_row = 0;                          // ring row written at step t (last wave)
 
+    // optional phase offset between co-resident workgroups (tuning knob)
+    if (stagger > 0 && (blockIdx.x & 1))
+      for (int z = 0; z < stagger; ++z) __builtin_amdgcn_s_sleep(1);
+
 #pragma unroll 1
     for (int32_t t = 0; t < T; ++t) {
+      // position 0's next symbols, read at the top of the step: sA/sB are
+      // read-only in the loop, so their LDS latency hides under the compute
+      int32_t nx0 = xpos0 + 1, nlap0 = lap0;
+      if (nx0 == P) { nx0 = 0; ++nlap0; }
+      const uint32_t ainj = sA[nx0];
+      const int32_t row0 = nlap0 * NW + w;
+      const uint32_t binj = (nlap0 >= 0 && row0 < lb) ? (uint32_t)sB[row0] : 0u;
       // ---- receive the wave-above record of step t-1
       uint4 rec[M];
       if (w == 0) {
@@ -476,15 +488,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       shift_pos<M>(svIyz, sel, mask0, pa.f_pair);
       shift_pos<M>(svM1, sel, mask0, 0u);
       // position 0 advances to u0 + 1
-      ++xpos0;
-      if (xpos0 == P) { xpos0 = 0; ++lap0; }
-      {
-        const uint32_t ainj = sA[xpos0];
-        const int32_t row0 = lap0 * NW + w;
-        const uint32_t binj = (lap0 >= 0 && row0 < lb) ? (uint32_t)sB[row0] : 0u;
-        shift_pos<M>(a, sel, mask0, ainj);
-        shift_pos<M>(b, sel, mask0, binj);
-      }
+      xpos0 = nx0;
+      lap0 = nlap0;
+      shift_pos<M>(a, sel, mask0, ainj);
+      shift_pos<M>(b, sel, mask0, binj);
 
       // ---- wave 0: fetch the record of step t + PD into the slot just consumed
       if (w == 0) {
@@ -748,8 +755,10 @@ static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                           (int)lds) != hipSuccess)
     return TSA_EDEVICE;
   const int grid = n < 65535 ? n : 65535;
+  int stagger = 0;
+  if (const char *e = getenv("TSA_PENCIL_STAGGER")) stagger = atoi(e);  // tuning knob
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * NW), lds, stream, d_seqs, d_offsets, n, g.P,
-                     g.R, lds_a, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, pa);
+                     g.R, lds_a, stagger, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, pa);
   return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
 }
 
