@@ -33,6 +33,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 
 #include "pencil_kernel.h"
@@ -304,7 +305,18 @@ __device__ __forceinline__ void cell_messages(
   }
 }
 
-template <int M, int NW>
+// Diagnostic stamps (separate build, never timed): per-wave sums of s_memtime
+// deltas over the step phases [receive, compute+send, shifts, barrier].
+#define TSA_STAMP(var)                                                             \
+  do {                                                                             \
+    if constexpr (STAMPS) {                                                        \
+      __builtin_amdgcn_sched_barrier(0);                                           \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory"); \
+      __builtin_amdgcn_sched_barrier(0);                                           \
+    }                                                                              \
+  } while (0)
+
+template <int M, int NW, bool STAMPS = false>
 __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restrict__ seqs,
                                                          const int64_t *__restrict__ offs,
                                                          int32_t n, int32_t P, int32_t R,
@@ -312,8 +324,11 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
                                                          int64_t ring_stride,
                                                          uint8_t *__restrict__ ring_base,
                                                          int32_t *__restrict__ scores,
-                                                         PencilArgs pa) {
+                                                         PencilArgs pa,
+                                                         unsigned long long *__restrict__ dbg) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0, st4 = 0;
+  unsigned long long acc[4] = {0, 0, 0, 0};
   constexpr int PAIR_BYTES = 64 * REC_BYTES;              // one pair's record, 1 KiB
   constexpr int SLOT_BYTES = M * PAIR_BYTES;
   uint8_t *xr = smem;                                     // [NW-1][2][M][64][16]
@@ -395,6 +410,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     if (stagger > 0 && (blockIdx.x & 1))
       for (int z = 0; z < stagger; ++z) __builtin_amdgcn_s_sleep(1);
 
+    TSA_STAMP(st0);
 #pragma unroll 1
     for (int32_t t = 0; t < T; ++t) {
       // position 0's next symbols, read at the top of the step: sA/sB are
@@ -431,6 +447,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       }
       // x == 1 at position k* = (t - w) mod P: its x-1 inputs are the x = 0 face
       // (EN_i==1&&EN==0 gating, src/PE_1cyc.v:164-178,196-202,212-218)
+      if constexpr (STAMPS) asm volatile("" ::"v"(rec[0].x), "v"(rec[M - 1].w));
+      TSA_STAMP(st1);
       x1_substitute<M>(xpos0, lane, pa, inIx, inIxy, inIxz, inM);
       uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
       cell_messages<M>(a, b, c, ones, pa, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx, oIy, oIz,
@@ -483,6 +501,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         svM2[i] = svM1[i];
         svM1[i] = rec[i].w;
       }
+      TSA_STAMP(st2);
       shift_pos<M>(shIxz1, sel, mask0, pa.f_pair);   // z = 0 face for position 0
       shift_pos<M>(shIz, sel, mask0, pa.f_single);
       shift_pos<M>(svIyz, sel, mask0, pa.f_pair);
@@ -505,10 +524,20 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         if (++st_row == R) st_row = 0;
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(M * STORE_SLACK) : "memory");
       }
+      TSA_STAMP(st3);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      TSA_STAMP(st4);
+      if constexpr (STAMPS) {
+        acc[0] += st1 - st0; acc[1] += st2 - st1; acc[2] += st3 - st2; acc[3] += st4 - st3;
+        st0 = st4;
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
+  if constexpr (STAMPS) {
+    if (blockIdx.x == 0 && lane == 0)
+      for (int q = 0; q < 4; ++q) dbg[w * 4 + q] = acc[q];
   }
 }
 
@@ -757,8 +786,28 @@ static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
   const int grid = n < 65535 ? n : 65535;
   int stagger = 0;
   if (const char *e = getenv("TSA_PENCIL_STAGGER")) stagger = atoi(e);  // tuning knob
+  if (getenv("TSA_PENCIL_STAMPS")) {  // diagnostic build: phase shares, printed to stderr
+    auto kst = pencil_kernel<M, NW, true>;
+    if (hipFuncSetAttribute((const void *)kst, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds) != hipSuccess)
+      return TSA_EDEVICE;
+    unsigned long long *dbg = nullptr, h[NW * 4];
+    if (hipMalloc(&dbg, sizeof(h)) != hipSuccess) return TSA_ENOMEM;
+    hipLaunchKernelGGL(kst, dim3(grid), dim3(64 * NW), lds, stream, d_seqs, d_offsets, n, g.P,
+                       g.R, lds_a, stagger, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores,
+                       pa, dbg);
+    if (hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+      return TSA_EDEVICE;
+    (void)hipFree(dbg);
+    for (int w = 0; w < NW; ++w)
+      fprintf(stderr, "STAMPS wave %2d recv %llu compute+send %llu shifts+dma %llu barrier %llu\n",
+              w, h[w * 4], h[w * 4 + 1], h[w * 4 + 2], h[w * 4 + 3]);
+    return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
+  }
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * NW), lds, stream, d_seqs, d_offsets, n, g.P,
-                     g.R, lds_a, stagger, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, pa);
+                     g.R, lds_a, stagger, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, pa,
+                     nullptr);
   return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
 }
 

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """A/B timing of kernel variants in ONE process, interleaved rounds (guide
 rule 24). Variants are environment knobs read by libtrialign at launch.
-  python tools/bench_variants.py --variants "TSA_PENCIL_NW=16" "TSA_PENCIL_NW=8" [--n 512 --L 256]
+  python tools/bench_variants.py --variants "TSA_PENCIL_NW=16" "TSA_PENCIL_NW=8,TSA_PENCIL_STAGGER=14"
+A variant is a comma-separated list of KEY=VALUE; every key named by any
+variant is unset before each run, so variants never inherit each other's knobs.
 Prints one JSON line per variant (median/min ms, GCUPS) to stdout."""
 import argparse
 import json
@@ -32,23 +34,26 @@ def main():
     d_scores = torch.zeros(n, dtype=torch.int32, device="cuda")
     p = tsa.TsaParams.default()
     ws = 0
+    keys = sorted({kv.split("=", 1)[0] for v in args.variants for kv in v.split(",") if kv})
+
+    def apply(v):
+        for k in keys:
+            os.environ.pop(k, None)
+        for kv in v.split(","):
+            if kv:
+                k, val = kv.split("=", 1)
+                os.environ[k] = val
+
     for v in args.variants:  # workspace depends on the knobs: take the max
-        k, val = v.split("=", 1)
-        old = os.environ.get(k)
-        os.environ[k] = val
+        apply(v)
         ws = max(ws, tsa.workspace_size(n, L, L, L, p, args.kernel))
-        if old is None:
-            del os.environ[k]
-        else:
-            os.environ[k] = old
     d_ws = torch.empty(ws, dtype=torch.uint8, device="cuda")
     st = torch.cuda.current_stream()
     times = {v: [] for v in args.variants}
     scores = {}
 
     def run(v):
-        k, val = v.split("=", 1)
-        os.environ[k] = val
+        apply(v)
         tsa.score_batch_async(d_seqs.data_ptr(), d_offs.data_ptr(), n, L, L, L, d_scores.data_ptr(),
                               d_ws.data_ptr(), ws, st.cuda_stream, p, args.kernel)
 
