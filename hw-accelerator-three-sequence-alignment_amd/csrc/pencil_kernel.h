@@ -14,6 +14,7 @@ bool pencil_shape_supported(int32_t max_la, int32_t max_lb, int32_t max_lc);
 size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc);
 int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                         int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
-                        int32_t *d_scores, void *d_ws, size_t ws_bytes, hipStream_t stream);
+                        const Range &bound, int32_t *d_scores, void *d_ws, size_t ws_bytes,
+                        hipStream_t stream);
 
 }  // namespace tsa

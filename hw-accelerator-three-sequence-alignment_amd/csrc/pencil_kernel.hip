@@ -54,11 +54,15 @@ constexpr int MAX_LA = 4096, MAX_LB = 4096;
 constexpr int REC_BYTES = 16;      // {Iy, Ixy, Iyz, best} packed pairs per lane
 constexpr int RING_EXTRA = 8;
 
+// Packed (both halves) constants. int16 form: two's complement; exact-f16 form
+// (helix kernel, F16): f16 bits, pair penalties and f_pair with the mismatch
+// folded in, h_* the 2^13-scaled score deltas and h_c3 the triple-score base.
 struct PencilArgs {
   uint32_t E, O, E2, OE, O2;    // packed penalties GE, GO, 2GE, GO+GE, 2GO
   uint32_t f_single, f_pair;    // face messages of an all-zero cell
   uint32_t dm, mm;              // match-mismatch, mismatch
   uint32_t s3_d1, s3_d0, s3_ne; // RTL: s3 = ne + eab*(d0 + ebc*d1)
+  uint32_t h_dm, h_d0, h_d1, h_c3;
   int32_t sop;                  // TSA_S3_SOP
 };
 
@@ -305,44 +309,135 @@ __device__ __forceinline__ void cell_messages(
   }
 }
 
-// Diagnostic stamps (separate build, never timed): per-wave sums of s_memtime
-// deltas over the step phases [receive, compute+send, shifts, barrier].
-#define TSA_STAMP(var)                                                             \
-  do {                                                                             \
-    if constexpr (STAMPS) {                                                        \
-      __builtin_amdgcn_sched_barrier(0);                                           \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory"); \
-      __builtin_amdgcn_sched_barrier(0);                                           \
-    }                                                                              \
-  } while (0)
+// The pk_mad operands must be VGPRs (inline asm "v"): pin them once, or hipcc
+// re-materialises them from SGPRs with a v_mov before every use.
+__device__ __forceinline__ PencilArgs pin_score_consts(const PencilArgs &pa) {
+  PencilArgs r = pa;
+  asm volatile("" : "+v"(r.dm), "+v"(r.mm), "+v"(r.s3_d1), "+v"(r.s3_d0), "+v"(r.s3_ne));
+  return r;
+}
 
-template <int M, int NW, bool STAMPS = false>
+// ---------------------------------------------------------------------------
+// Exact-f16 arithmetic for the helix kernel. Every DP value is an integer; when
+// the host proves all of them (and every candidate) lie in [-2048, 2048]
+// (trialign_api.hip:pencil_exact), IEEE f16 add/fma/maximum on them are exact,
+// and CDNA4's v_pk_maximum3_f16 folds two packed maxes into one instruction.
+// Symbol codes are one-hot at bits 11..14 (0x800 << s), so min_u16(a & b, 0x800)
+// is 0x0800 = f16 2^-13 on a match and 0 otherwise; the match-mismatch deltas
+// are pre-scaled by 2^13 so a single v_pk_fma_f16 adds a pair score. The
+// mismatch score of each pair target is folded into the penalties its
+// messages carry (Ep = GE - mismatch, Op = GO - mismatch, and f_pair).
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2 H(uint32_t v) { return __builtin_bit_cast(h2, v); }
+__device__ __forceinline__ uint32_t U(h2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ h2 hmax(h2 a, h2 b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ h2 hmax3(h2 a, h2 b, h2 c) { return hmax(hmax(a, b), c); }
+__device__ __forceinline__ h2 hfma(h2 a, h2 b, h2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ uint32_t umin2(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(us2, a),
+                                                                 __builtin_bit_cast(us2, b)));
+}
+constexpr uint32_t SYM0 = 0x800u;  // helix symbol codes: SYM0 << s
+
+template <int M>
+__device__ __forceinline__ void cell_messages_f16(
+    const uint32_t (&a)[M], const uint32_t (&b)[M], const uint32_t (&c)[M], uint32_t Q,
+    const PencilArgs &pa, const uint32_t (&inIx)[M], const uint32_t (&inIy)[M],
+    const uint32_t (&inIz)[M], const uint32_t (&inIxy)[M], const uint32_t (&inIyz)[M],
+    const uint32_t (&inIxz)[M], const uint32_t (&inM)[M], uint32_t (&nIx)[M], uint32_t (&oIy)[M],
+    uint32_t (&oIz)[M], uint32_t (&oIxy)[M], uint32_t (&oIyz)[M], uint32_t (&oIxz)[M],
+    uint32_t (&oBest)[M]) {
+  const h2 DM = H(pa.h_dm), E = H(pa.E), O = H(pa.O), E2 = H(pa.E2), OE = H(pa.OE), O2 = H(pa.O2);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const uint32_t ab = a[i] & b[i];
+    const h2 eab = H(umin2(ab, Q)), eac = H(umin2(a[i] & c[i], Q)), ebc = H(umin2(b[i] & c[i], Q));
+    const h2 sXY = hfma(eab, DM, H(inIxy[i]));  // src/PE_1cyc.v:159-161 (+mismatch folded)
+    const h2 sYZ = hfma(ebc, DM, H(inIyz[i]));
+    const h2 sXZ = hfma(eac, DM, H(inIxz[i]));
+    h2 sM;                                       // src/PE_1cyc.v:162
+    if (pa.sop) {
+      sM = hfma(eab, DM, hfma(ebc, DM, hfma(eac, DM, H(inM[i])))) + H(pa.h_c3);
+    } else {  // RTL: ne + eab*(d0 + ebc*d1) = ne + d0*[a=b] + d1*[a=b=c]
+      const h2 e3 = H(umin2(ab & c[i], Q));
+      sM = hfma(e3, H(pa.h_d1), hfma(eab, H(pa.h_d0), H(inM[i]))) + H(pa.h_c3);
+    }
+    const h2 sX = H(inIx[i]), sY = H(inIy[i]), sZ = H(inIz[i]);
+    const h2 pYZ = hmax(sY, sZ), pXZ = hmax(sX, sZ), pXY = hmax(sX, sY);
+    const h2 A1 = hmax3(pYZ, sXY, sXZ);  // Ix  <- {Iy,Iz,Ixy,Ixz} at GO+GE
+    const h2 A2 = hmax3(pXZ, sXY, sYZ);  // Iy  <- {Ix,Iz,Ixy,Iyz}
+    const h2 A3 = hmax3(pXY, sYZ, sXZ);  // Iz  <- {Ix,Iy,Iyz,Ixz}
+    const h2 B1 = hmax(sM, sYZ);         // Ix  <- {M,Iyz} at 2GO
+    const h2 B2 = hmax(sM, sXZ);
+    const h2 B3 = hmax(sM, sXY);
+    const h2 C1 = hmax(pXY, sXY);        // Ixy <- {Ix,Iy,Ixy} at GE
+    const h2 C2 = hmax(pYZ, sYZ);
+    const h2 C3 = hmax(pXZ, sXZ);
+    const h2 D1 = hmax3(B1, sZ, sXZ);    // Ixy <- {M,Iz,Iyz,Ixz} at GO
+    const h2 D2 = hmax3(B2, sX, sXY);
+    const h2 D3 = hmax3(B3, sY, sYZ);
+    oBest[i] = U(hmax3(A1, B1, sX));     // MAX7 of the states
+    nIx[i] = U(hmax3(sX - E2, A1 - OE, B1 - O2));
+    oIy[i] = U(hmax3(sY - E2, A2 - OE, B2 - O2));
+    oIz[i] = U(hmax3(sZ - E2, A3 - OE, B3 - O2));
+    oIxy[i] = U(hmax(C1 - E, D1 - O));
+    oIyz[i] = U(hmax(C2 - E, D2 - O));
+    oIxz[i] = U(hmax(C3 - E, D3 - O));
+  }
+}
+
+// Shift a packed per-position value one position up the helix (k <- k-1):
+// lanes >= 1 take lane-1's pair as is; lane 0 takes (pair i-1).hi and
+// (pair i).lo of lane 63; position 0 (lane 0, pair 0, lo) gets the z = 0 face.
+template <int M>
+__device__ __forceinline__ void zshift(uint32_t (&v)[M], const uint32_t (&src)[M], uint32_t sel,
+                                       uint32_t mask0, uint32_t face) {
+  uint32_t r[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) r[i] = ror1(src[i]);
+#pragma unroll
+  for (int i = 0; i < M; ++i) v[i] = __builtin_amdgcn_perm(r[i], r[(i + M - 1) % M], sel);
+  v[0] = bfi(mask0, face, v[0]);
+}
+
+// ---------------------------------------------------------------------------
+// Helix kernel: one workgroup per triple (grid-stride over the batch).
+//   LDS: xr  [NW-1][2][M][64][16]  wave w -> w+1 records {Iy, Ixy, Iyz, best}
+//        xr0 [PD][M][64][16]       ring rows prefetched for wave 0 (LDS-DMA)
+//        sA2 [P+256] u32           A codes for positions k and k+64 of one pair
+//        sB  [LB] u32              B code, both halves
+//        fin [M][64] u32           best of the final step (wave w_f)
+// F16 selects the exact-f16 arithmetic above, else the int16 form.
+template <int M, int NW, bool F16>
 __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restrict__ seqs,
                                                          const int64_t *__restrict__ offs,
                                                          int32_t n, int32_t P, int32_t R,
-                                                         int32_t lds_a, int32_t stagger,
+                                                         int32_t lds_a, int32_t lds_b,
                                                          int64_t ring_stride,
                                                          uint8_t *__restrict__ ring_base,
                                                          int32_t *__restrict__ scores,
-                                                         PencilArgs pa,
-                                                         unsigned long long *__restrict__ dbg) {
+                                                         PencilArgs pa) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0, st4 = 0;
-  unsigned long long acc[4] = {0, 0, 0, 0};
-  constexpr int PAIR_BYTES = 64 * REC_BYTES;              // one pair's record, 1 KiB
+  constexpr int PAIR_BYTES = 64 * REC_BYTES;  // one pair's record, 1 KiB
   constexpr int SLOT_BYTES = M * PAIR_BYTES;
-  uint8_t *xr = smem;                                     // [NW-1][2][M][64][16]
-  uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT_BYTES;          // [PD][M][64][16]
-  uint8_t *sA = xr0 + PD * SLOT_BYTES;                    // [lds_a >= P] one-hot A
-  uint8_t *sB = sA + lds_a;                               // [>= max LB] one-hot B
+  constexpr int ZT = 128 * M;
+  uint8_t *xr = smem;
+  uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT_BYTES;
+  uint32_t *sA2 = (uint32_t *)(xr0 + PD * SLOT_BYTES);
+  uint32_t *sB = (uint32_t *)((uint8_t *)sA2 + lds_a);
+  uint32_t *fin = (uint32_t *)((uint8_t *)sB + lds_b);
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t sel = lane == 0 ? 0x05040302u : 0x07060504u;
   const uint32_t mask0 = lane == 0 ? 0x0000FFFFu : 0u;
-  uint32_t ones = 0x00010001u;
-  asm volatile("" : "+v"(ones));  // keep it in a VGPR (VOP3P operand)
-  constexpr int ZT = 128 * M;
+  uint32_t ones = F16 ? 0x08000800u : 0x00010001u;  // f16: match indicator 2^-13
+  asm volatile("" : "+v"(ones));                     // keep it in a VGPR (VOP3P operand)
+  const PencilArgs pv = F16 ? pa : pin_score_consts(pa);
+  // a[i] of this lane at step t is sA2[(t-w) mod P + 256 - lane - 128 i]
+  const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
+                          4u * (uint32_t)(256 - lane - 128 * (M - 1));
 
   for (int tri = blockIdx.x; tri < n; tri += gridDim.x) {
     const int64_t o0 = offs[3 * (int64_t)tri], o1 = offs[3 * (int64_t)tri + 1];
@@ -350,10 +445,15 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     const int32_t la = (int32_t)(o1 - o0), lb = (int32_t)(o2 - o1), lc = (int32_t)(o3 - o2);
     uint8_t *ring = ring_base + (int64_t)blockIdx.x * ring_stride;
 
-    // ---- stage one-hot A (padded to P) and B; fill the ring with face records
-    for (int i = threadIdx.x; i < P; i += 64 * NW)
-      sA[i] = i < la ? (uint8_t)(1u << (seqs[o0 + i] & 3)) : 0;
-    for (int i = threadIdx.x; i < lb; i += 64 * NW) sB[i] = (uint8_t)(1u << (seqs[o1 + i] & 3));
+    // ---- stage A codes (padded to P, pairs k/k+64) and B; face records in the ring
+    for (int j = threadIdx.x; j < P + 256; j += 64 * NW) {
+      const int x0 = ((j - 256) % P + P) % P, x1 = ((j - 320) % P + P) % P;
+      const uint32_t c0 = x0 < la ? SYM0 << (seqs[o0 + x0] & 3) : 0u;
+      const uint32_t c1 = x1 < la ? SYM0 << (seqs[o0 + x1] & 3) : 0u;
+      sA2[j] = c0 | (c1 << 16);
+    }
+    for (int i = threadIdx.x; i < lb; i += 64 * NW)
+      sB[i] = (SYM0 << (seqs[o1 + i] & 3)) * 0x00010001u;
     {
       const uint4 face = make_uint4(pa.f_single, pa.f_pair, pa.f_pair, 0u);
       const int64_t n16 = (int64_t)R * M * 64;
@@ -362,33 +462,27 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
 
-    // ---- per-position registers
-    uint32_t a[M], b[M], c[M];
-    uint32_t oIx[M], shIz[M], shIxz1[M], shIxz2[M], svIxy[M], svIyz[M], svM1[M], svM2[M];
+    // ---- per-position registers (arrays [2] alternate roles between even/odd steps)
+    uint32_t b[M], c[M];
+    uint32_t oIx[M], shIz[M], svIxy[M], svIyz[M], shIxz[2][M], svM[2][M];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
       const int k0 = lane + 128 * i, k1 = lane + 64 + 128 * i;
-      const uint32_t c0 = k0 < lc ? 1u << (seqs[o2 + k0] & 3) : 0u;
-      const uint32_t c1 = k1 < lc ? 1u << (seqs[o2 + k1] & 3) : 0u;
+      const uint32_t c0 = k0 < lc ? SYM0 << (seqs[o2 + k0] & 3) : 0u;
+      const uint32_t c1 = k1 < lc ? SYM0 << (seqs[o2 + k1] & 3) : 0u;
       c[i] = c0 | (c1 << 16);
-      // symbols at step 0: position k is at u = -w-k (x index (u mod P))
-      const int x0 = ((-w - k0) % P + P) % P, x1 = ((-w - k1) % P + P) % P;
-      a[i] = (uint32_t)sA[x0] | ((uint32_t)sA[x1] << 16);
-      // only position 0 of wave 0 has started (u = 0, row 1); others are u < 0
-      b[i] = (i == 0 && w == 0 && lane == 0) ? (uint32_t)sB[0] : 0u;
+      b[i] = 0;  // set when a position reaches x = 1 of its lap
       oIx[i] = pa.f_single;
       shIz[i] = pa.f_single;
-      shIxz1[i] = shIxz2[i] = pa.f_pair;
+      shIxz[0][i] = shIxz[1][i] = pa.f_pair;
       svIxy[i] = svIyz[i] = pa.f_pair;
-      svM1[i] = svM2[i] = 0;
+      svM[0][i] = svM[1][i] = 0;
     }
     // position-0 bookkeeping (wave-uniform): u0 = t - w
-    int32_t xpos0 = (P - (w % P)) % P;      // (t - w) mod P at t = 0
-    int32_t lap0 = w == 0 ? 0 : -1;         // floor((t - w) / P)
-    // final cell (la, lb, lc)
+    int32_t xpos0 = (P - (w % P)) % P;  // (t - w) mod P at t = 0
+    int32_t lap0 = w == 0 ? 0 : -1;     // floor((t - w) / P)
     const int32_t lap_f = (lb - 1) / NW, w_f = (lb - 1) % NW, k_f = lc - 1;
-    const int32_t t_f = lap_f * P + (la - 1) + w_f + k_f;
-    const int32_t l_f = k_f & 63, i_f = k_f >> 7, h_f = (k_f >> 6) & 1;
+    const int32_t t_f = lap_f * P + (la - 1) + w_f + k_f;  // final cell (la, lb, lc)
     const int32_t T = t_f + 1;
 
     // wave 0: prime the LDS-DMA pipeline (ring row of step s = s - P + NW - 1)
@@ -406,20 +500,20 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     int32_t dma_row = ((PD - lag) % R + R) % R;  // ring row for step t + PD
     int32_t st_row = 0;                          // ring row written at step t (last wave)
 
-    // optional phase offset between co-resident workgroups (tuning knob)
-    if (stagger > 0 && (blockIdx.x & 1))
-      for (int z = 0; z < stagger; ++z) __builtin_amdgcn_s_sleep(1);
-
-    TSA_STAMP(st0);
-#pragma unroll 1
-    for (int32_t t = 0; t < T; ++t) {
-      // position 0's next symbols, read at the top of the step: sA/sB are
-      // read-only in the loop, so their LDS latency hides under the compute
-      int32_t nx0 = xpos0 + 1, nlap0 = lap0;
-      if (nx0 == P) { nx0 = 0; ++nlap0; }
-      const uint32_t ainj = sA[nx0];
-      const int32_t row0 = nlap0 * NW + w;
-      const uint32_t binj = (nlap0 >= 0 && row0 < lb) ? (uint32_t)sB[row0] : 0u;
+    // One step; PH = t & 1 picks the register roles and the LDS record slots.
+    auto step = [&](auto ph, int32_t t) {
+      constexpr int PH = decltype(ph)::value;
+      // this step's A codes (LDS table) and the B code of position x = 1
+      uint32_t a[M];
+      {
+        const uint32_t va = a_lane + 4u * (uint32_t)xpos0;
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+          a[i] = *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t)(
+              va + 512u * (uint32_t)(M - 1 - i));
+      }
+      const int32_t row0 = lap0 * NW + w;
+      const uint32_t binj = (lap0 >= 0 && row0 < lb) ? sB[row0] : 0u;
       // ---- receive the wave-above record of step t-1
       uint4 rec[M];
       if (w == 0) {
@@ -428,12 +522,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll
         for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
       } else {
-        const uint8_t *src = xr + ((w - 1) * 2 + ((t - 1) & 1)) * SLOT_BYTES + lane * REC_BYTES;
+        const uint8_t *src = xr + ((w - 1) * 2 + (PH ^ 1)) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
         for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
       }
-
-      // ---- inputs (messages into this cell)
       uint32_t inIx[M], inIy[M], inIz[M], inIxy[M], inIyz[M], inIxz[M], inM[M];
 #pragma unroll
       for (int i = 0; i < M; ++i) {
@@ -442,21 +534,45 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         inIz[i] = shIz[i];
         inIxy[i] = svIxy[i];
         inIyz[i] = svIyz[i];
-        inIxz[i] = shIxz2[i];
-        inM[i] = svM2[i];
+        inIxz[i] = shIxz[PH][i];
+        inM[i] = svM[PH][i];
       }
-      // x == 1 at position k* = (t - w) mod P: its x-1 inputs are the x = 0 face
-      // (EN_i==1&&EN==0 gating, src/PE_1cyc.v:164-178,196-202,212-218)
-      if constexpr (STAMPS) asm volatile("" ::"v"(rec[0].x), "v"(rec[M - 1].w));
-      TSA_STAMP(st1);
-      x1_substitute<M>(xpos0, lane, pa, inIx, inIxy, inIxz, inM);
+      // ---- x == 1 at position k* = (t - w) mod P: its x-1 inputs are the x = 0
+      // face (EN_i==1&&EN==0 gating, src/PE_1cyc.v:164-178,196-202,212-218), and
+      // it starts row lap0*NW+w+1, whose B symbol it takes here.
+      if (xpos0 < ZT) {
+        const uint32_t hm = (xpos0 >> 6) & 1 ? 0xFFFF0000u : 0x0000FFFFu;
+        const uint32_t m1 = lane == (xpos0 & 63) ? hm : 0u;
+        const int is = xpos0 >> 7;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          if (i == is) {
+            inIx[i] = bfi(m1, pa.f_single, inIx[i]);
+            inIxy[i] = bfi(m1, pa.f_pair, inIxy[i]);
+            inIxz[i] = bfi(m1, pa.f_pair, inIxz[i]);
+            inM[i] = bfi(m1, 0u, inM[i]);
+            b[i] = bfi(m1, binj, b[i]);
+          }
+        }
+      }
       uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
-      cell_messages<M>(a, b, c, ones, pa, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx, oIy, oIz,
-                       oIxy, oIyz, oIxz, oBest);
+      if constexpr (F16)
+        cell_messages_f16<M>(a, b, c, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx,
+                             oIy, oIz, oIxy, oIyz, oIxz, oBest);
+      else
+        cell_messages<M>(a, b, c, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx, oIy,
+                         oIz, oIxy, oIyz, oIxz, oBest);
+
+      // ---- the final cell (src/TriAlign_1cyc.v:141-142,342-345) is in wave w_f's
+      // last step; it is read back after the loop
+      if (t == T - 1 && w == w_f) {
+#pragma unroll
+        for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
+      }
 
       // ---- send this step's record to the wave below (or the ring)
       if (w < NW - 1) {
-        uint8_t *dst = xr + (w * 2 + (t & 1)) * SLOT_BYTES + lane * REC_BYTES;
+        uint8_t *dst = xr + (w * 2 + PH) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
         for (int i = 0; i < M; ++i)
           lds_write16(dst + i * PAIR_BYTES, make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
@@ -480,37 +596,21 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll
         for (int i = 0; i < M; ++i) dst[i * 64] = make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]);
       }
-
-      // ---- final cell (src/TriAlign_1cyc.v:141-142,342-345)
-      if (t == t_f && w == w_f) {
-        uint32_t v = oBest[0];
-#pragma unroll
-        for (int i = 1; i < M; ++i) if (i == i_f) v = oBest[i];
-        if (lane == l_f) scores[tri] = (int32_t)(int16_t)(h_f ? (v >> 16) : (v & 0xFFFF));
-      }
-
       // ---- advance the systolic registers
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         oIx[i] = nIx[i];
-        shIxz2[i] = shIxz1[i];
-        shIxz1[i] = oIxz[i];
-        shIz[i] = oIz[i];
         svIxy[i] = rec[i].y;
-        svIyz[i] = rec[i].z;
-        svM2[i] = svM1[i];
-        svM1[i] = rec[i].w;
       }
-      TSA_STAMP(st2);
-      shift_pos<M>(shIxz1, sel, mask0, pa.f_pair);   // z = 0 face for position 0
-      shift_pos<M>(shIz, sel, mask0, pa.f_single);
-      shift_pos<M>(svIyz, sel, mask0, pa.f_pair);
-      shift_pos<M>(svM1, sel, mask0, 0u);
+      uint32_t rz[M], rw[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) { rz[i] = rec[i].z; rw[i] = rec[i].w; }
+      zshift<M>(shIxz[PH], oIxz, sel, mask0, pa.f_pair);  // z = 0 face for position 0
+      zshift<M>(shIz, oIz, sel, mask0, pa.f_single);
+      zshift<M>(svIyz, rz, sel, mask0, pa.f_pair);
+      zshift<M>(svM[PH], rw, sel, mask0, 0u);
       // position 0 advances to u0 + 1
-      xpos0 = nx0;
-      lap0 = nlap0;
-      shift_pos<M>(a, sel, mask0, ainj);
-      shift_pos<M>(b, sel, mask0, binj);
+      if (++xpos0 == P) { xpos0 = 0; ++lap0; }
 
       // ---- wave 0: fetch the record of step t + PD into the slot just consumed
       if (w == 0) {
@@ -524,20 +624,25 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         if (++st_row == R) st_row = 0;
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(M * STORE_SLACK) : "memory");
       }
-      TSA_STAMP(st3);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      TSA_STAMP(st4);
-      if constexpr (STAMPS) {
-        acc[0] += st1 - st0; acc[1] += st2 - st1; acc[2] += st3 - st2; acc[3] += st4 - st3;
-        st0 = st4;
-      }
+    };
+
+    int32_t t = 0;
+#pragma unroll 1
+    for (; t + 1 < T; t += 2) {
+      step(std::integral_constant<int, 0>{}, t);
+      step(std::integral_constant<int, 1>{}, t + 1);
     }
+    if (t < T) step(std::integral_constant<int, 0>{}, t);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-  }
-  if constexpr (STAMPS) {
-    if (blockIdx.x == 0 && lane == 0)
-      for (int q = 0; q < 4; ++q) dbg[w * 4 + q] = acc[q];
+    if (threadIdx.x == 0) {
+      const int32_t l_f = k_f & 63, i_f = k_f >> 7, h_f = (k_f >> 6) & 1;
+      const uint32_t v = fin[i_f * 64 + l_f];
+      const uint16_t hb = (uint16_t)(h_f ? (v >> 16) : (v & 0xFFFF));
+      scores[tri] = F16 ? (int32_t)(float)__builtin_bit_cast(_Float16, hb) : (int32_t)(int16_t)hb;
+    }
+    __syncthreads();
   }
 }
 
@@ -578,6 +683,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
   const uint32_t mask0 = lane == 0 ? 0x0000FFFFu : 0u;
   uint32_t ones = 0x00010001u;
   asm volatile("" : "+v"(ones));
+  const PencilArgs pv = pin_score_consts(pa);
 
   const int32_t tri = blockIdx.x / G, L = blockIdx.x % G;
   const int64_t o0 = offs[3 * (int64_t)tri], o1 = offs[3 * (int64_t)tri + 1];
@@ -681,7 +787,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     }
     x1_substitute<M>(t - w, lane, pa, inIx, inIxy, inIxz, inM);
     uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
-    cell_messages<M>(a, b, c, ones, pa, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx, oIy, oIz,
+    cell_messages<M>(a, b, c, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx, oIy, oIz,
                      oIxy, oIyz, oIxz, oBest);
 
     if (w < NW - 1) {
@@ -748,66 +854,82 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
 }
 
 
-static PencilArgs make_args(const KParams &kp) {
-  auto pk = [](int32_t v) { return ((uint32_t)(uint16_t)(int16_t)v) * 0x00010001u; };
+static uint32_t pk16(int32_t v) { return ((uint32_t)(uint16_t)(int16_t)v) * 0x00010001u; }
+static uint32_t pkh(double v) {  // both halves = f16(v); v exactly representable
+  const _Float16 h = (_Float16)v;
+  uint16_t bits;
+  memcpy(&bits, &h, 2);
+  return (uint32_t)bits * 0x00010001u;
+}
+
+static PencilArgs make_args(const KParams &kp, bool f16) {
   const int32_t GE = kp.pen[SIXY][SIX], GO = kp.pen[SIXY][SM];  // Ixy row: Ix = GE, M = GO
-  PencilArgs a;
-  a.E = pk(GE);
-  a.O = pk(GO);
-  a.E2 = pk(2 * GE);
-  a.OE = pk(GO + GE);
-  a.O2 = pk(2 * GO);
   int32_t fs = -kp.pen[SIX][0], fp = -kp.pen[SIXY][0];
   for (int s = 0; s < 7; ++s) {
     fs = std::max(fs, -kp.pen[SIX][s]);
     fp = std::max(fp, -kp.pen[SIXY][s]);
   }
-  a.f_single = pk(fs);
-  a.f_pair = pk(fp);
-  a.dm = pk(kp.match - kp.mismatch);
-  a.mm = pk(kp.mismatch);
-  a.s3_d1 = pk(kp.s3_eq - kp.s3_ab);
-  a.s3_d0 = pk(kp.s3_ab - kp.s3_ne);
-  a.s3_ne = pk(kp.s3_ne);
+  PencilArgs a;
+  memset(&a, 0, sizeof(a));
   a.sop = kp.s3_mode == TSA_S3_SOP;
+  if (!f16) {
+    a.E = pk16(GE);
+    a.O = pk16(GO);
+    a.E2 = pk16(2 * GE);
+    a.OE = pk16(GO + GE);
+    a.O2 = pk16(2 * GO);
+    a.f_single = pk16(fs);
+    a.f_pair = pk16(fp);
+    a.dm = pk16(kp.match - kp.mismatch);
+    a.mm = pk16(kp.mismatch);
+    a.s3_d1 = pk16(kp.s3_eq - kp.s3_ab);
+    a.s3_d0 = pk16(kp.s3_ab - kp.s3_ne);
+    a.s3_ne = pk16(kp.s3_ne);
+    return a;
+  }
+  const int32_t mm = kp.mismatch;
+  a.E = pkh(GE - mm);
+  a.O = pkh(GO - mm);
+  a.E2 = pkh(2 * GE);
+  a.OE = pkh(GO + GE);
+  a.O2 = pkh(2 * GO);
+  a.f_single = pkh(fs);
+  a.f_pair = pkh(fp + mm);
+  a.h_dm = pkh((kp.match - mm) * 8192.0);
+  a.h_d0 = pkh((kp.s3_ab - kp.s3_ne) * 8192.0);
+  a.h_d1 = pkh((kp.s3_eq - kp.s3_ab) * 8192.0);
+  a.h_c3 = pkh(a.sop ? 3.0 * mm : (double)kp.s3_ne);
   return a;
 }
 
-template <int M, int NW>
+// Exact-f16 arithmetic applies when every value and candidate is an integer in
+// [-2048, 2048] (value bound + PENCIL_MARGIN) and the scaled deltas fit f16.
+static bool use_f16(const KParams &kp, const Range &r) {
+  if (const char *e = getenv("TSA_PENCIL_ARITH"))  // tuning / test knob
+    if (!strcmp(e, "i16")) return false;
+  auto small = [](int64_t v) { return v >= -7 && v <= 7; };
+  auto fits = [](int64_t v) { return v >= -2048 && v <= 2048; };
+  return r.lo - PENCIL_MARGIN >= -2048 && r.hi + PENCIL_MARGIN <= 2048 &&
+         small((int64_t)kp.match - kp.mismatch) && small((int64_t)kp.s3_ab - kp.s3_ne) &&
+         small((int64_t)kp.s3_eq - kp.s3_ab) && fits(kp.mismatch) && fits(kp.s3_ne) &&
+         fits(3LL * kp.mismatch);
+}
+
+template <int M, int NW, bool F16>
 static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                     int32_t max_lb, const PencilGeom &g, int32_t *d_scores, void *d_ws,
                     const PencilArgs &pa, hipStream_t stream) {
-  const int32_t lds_a = (g.P + 15) & ~15, lds_b = (max_lb + 15) & ~15;
-  const size_t lds = (size_t)(NW - 1) * 2 * M * 1024 + (size_t)PD * M * 1024 + lds_a + lds_b;
-  auto kfn = pencil_kernel<M, NW>;
+  const int32_t lds_a = 4 * (g.P + 256), lds_b = 4 * ((max_lb + 3) & ~3);
+  const size_t lds = (size_t)(NW - 1) * 2 * M * 1024 + (size_t)PD * M * 1024 + lds_a + lds_b +
+                     (size_t)M * 64 * 4;
+  auto kfn = pencil_kernel<M, NW, F16>;
+  if (lds > 160 * 1024) return TSA_EINVAL;
   if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return TSA_EDEVICE;
   const int grid = n < 65535 ? n : 65535;
-  int stagger = 0;
-  if (const char *e = getenv("TSA_PENCIL_STAGGER")) stagger = atoi(e);  // tuning knob
-  if (getenv("TSA_PENCIL_STAMPS")) {  // diagnostic build: phase shares, printed to stderr
-    auto kst = pencil_kernel<M, NW, true>;
-    if (hipFuncSetAttribute((const void *)kst, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds) != hipSuccess)
-      return TSA_EDEVICE;
-    unsigned long long *dbg = nullptr, h[NW * 4];
-    if (hipMalloc(&dbg, sizeof(h)) != hipSuccess) return TSA_ENOMEM;
-    hipLaunchKernelGGL(kst, dim3(grid), dim3(64 * NW), lds, stream, d_seqs, d_offsets, n, g.P,
-                       g.R, lds_a, stagger, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores,
-                       pa, dbg);
-    if (hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, stream) != hipSuccess ||
-        hipStreamSynchronize(stream) != hipSuccess)
-      return TSA_EDEVICE;
-    (void)hipFree(dbg);
-    for (int w = 0; w < NW; ++w)
-      fprintf(stderr, "STAMPS wave %2d recv %llu compute+send %llu shifts+dma %llu barrier %llu\n",
-              w, h[w * 4], h[w * 4 + 1], h[w * 4 + 2], h[w * 4 + 3]);
-    return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
-  }
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * NW), lds, stream, d_seqs, d_offsets, n, g.P,
-                     g.R, lds_a, stagger, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, pa,
-                     nullptr);
+                     g.R, lds_a, lds_b, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, pa);
   return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
 }
 
@@ -831,13 +953,14 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
 
 int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                         int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
-                        int32_t *d_scores, void *d_ws, size_t ws_bytes, hipStream_t stream) {
+                        const Range &bound, int32_t *d_scores, void *d_ws, size_t ws_bytes,
+                        hipStream_t stream) {
   if (n <= 0) return TSA_OK;
   if (!pencil_shape_ok(max_la, max_lb, max_lc)) return TSA_EINVAL;
   if (use_lap_mode(n, max_lb)) {
     const LapGeom lg = lap_geom(n, max_la, max_lb, max_lc);
     if (ws_bytes < lg.flag_bytes + lg.yf_bytes) return TSA_ENOMEM;
-    const PencilArgs pa = make_args(kp);
+    const PencilArgs pa = make_args(kp, false);
 #define TSA_LAP(MM, NN) launch_lap<MM, NN>(d_seqs, d_offsets, n, max_la, lg, d_scores, d_ws, pa, stream)
     if (pencil_pairs(max_lc) == 1)
       return lg.NW == 4 ? TSA_LAP(1, 4) : lg.NW == 8 ? TSA_LAP(1, 8) : TSA_LAP(1, 16);
@@ -847,14 +970,17 @@ int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t
   const PencilGeom g = pencil_geom(max_la, max_lc);
   const int32_t grid = n < 65535 ? n : 65535;
   if (ws_bytes < (size_t)grid * (size_t)g.ring_bytes_per_triple) return TSA_ENOMEM;
-  const PencilArgs pa = make_args(kp);
+  const bool f16 = use_f16(kp, bound);
+  const PencilArgs pa = make_args(kp, f16);
   int nw = PENCIL_NW_DEFAULT;
   if (const char *e = getenv("TSA_PENCIL_NW")) nw = atoi(e) == 8 ? 8 : 16;  // tuning knob
-  if (g.M == 1)
-    return nw == 8 ? launch_m<1, 8>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_ws, pa, stream)
-                   : launch_m<1, 16>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_ws, pa, stream);
-  return nw == 8 ? launch_m<2, 8>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_ws, pa, stream)
-                 : launch_m<2, 16>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_ws, pa, stream);
+#define TSA_HELIX(MM, NN, FF) \
+  launch_m<MM, NN, FF>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_ws, pa, stream)
+#define TSA_HELIX_F(MM, NN) (f16 ? TSA_HELIX(MM, NN, true) : TSA_HELIX(MM, NN, false))
+  if (g.M == 1) return nw == 8 ? TSA_HELIX_F(1, 8) : TSA_HELIX_F(1, 16);
+  return nw == 8 ? TSA_HELIX_F(2, 8) : TSA_HELIX_F(2, 16);
+#undef TSA_HELIX_F
+#undef TSA_HELIX
 }
 
 }  // namespace tsa

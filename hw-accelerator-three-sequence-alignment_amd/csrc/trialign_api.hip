@@ -199,8 +199,8 @@ static int launch_kind(int kind, const uint8_t *d_seqs, const int64_t *d_off, in
   if (kind == TSA_KERNEL_PLANE)
     return plane_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp, d_scores, d_final7,
                               ws, ws_bytes, s);
-  return pencil_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp, d_scores, ws,
-                             ws_bytes, s);
+  return pencil_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp,
+                             value_bound(p, max_la, max_lb, max_lc), d_scores, ws, ws_bytes, s);
 }
 
 #define HIPCHK(x)                                   \
