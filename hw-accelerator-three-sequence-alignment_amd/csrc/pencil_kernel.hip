@@ -45,7 +45,7 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 // waves (= DP rows) per lap: 16 (one 1024-thread WG per CU) or 8 (two WGs
 // per CU, so one computes while the other waits at its per-step barrier)
-constexpr int PENCIL_NW_DEFAULT = 16;
+constexpr int PENCIL_NW_DEFAULT = 8;
 constexpr int PD = 8;              // LDS-DMA prefetch distance of wave 0, steps
 constexpr int LPD = 4;             // prefetch distance of the lap kernel (cross-CU hand-off)
 constexpr int STORE_SLACK = 4;     // last wave keeps <= this many steps of stores in flight
@@ -62,7 +62,8 @@ struct PencilArgs {
   uint32_t f_single, f_pair;    // face messages of an all-zero cell
   uint32_t dm, mm;              // match-mismatch, mismatch
   uint32_t s3_d1, s3_d0, s3_ne; // RTL: s3 = ne + eab*(d0 + ebc*d1)
-  uint32_t h_dm, h_d0, h_d1, h_c3;
+  uint32_t h_dm, h_c3;           // 2^13 (match-mismatch); RTL ne
+  uint32_t h_sbc, h_k0, h_kd;     // per-row registers, see cell_messages_f16
   int32_t sop;                  // TSA_S3_SOP
 };
 
@@ -170,6 +171,13 @@ __device__ __forceinline__ uint32_t pk_eq1(uint32_t a, uint32_t b, uint32_t ones
 __device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
   return (mask & a) | (~mask & b);
 }
+// one v_bfi_b32 (hipcc otherwise splits a group of bfi's with a shared mask
+// into v_not + v_and + v_and_or)
+__device__ __forceinline__ uint32_t vbfi(uint32_t mask, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "v"(a), "v"(b));
+  return r;
+}
 // One LDS-DMA of 16 B per lane: LDS[m0 + lane*16] <- *gsrc (sc1: bypass L1).
 // Issued from inline asm so that hipcc does not treat it as an in-flight LDS
 // write and drain vmcnt(0) before every ds_read of the step loop; the
@@ -261,7 +269,7 @@ __device__ __forceinline__ void x1_substitute(int ks, int lane, const PencilArgs
 // One step of M packed cell pairs: scores (src/PE_1cyc.v:159-162) on one-hot
 // symbols, the 7 states, and the 7 outgoing messages max_s(S[s] - P[T][s])
 // (src/PE_1cyc.v:164-218) grouped by equal penalty; oBest = MAX7 of the states.
-template <int M>
+template <int M, int SOPM = -1>  // SOPM: 0 RTL, 1 SOP, -1 read pa.sop
 __device__ __forceinline__ void cell_messages(
     const uint32_t (&a)[M], const uint32_t (&b)[M], const uint32_t (&c)[M], uint32_t ones,
     const PencilArgs &pa, const uint32_t (&inIx)[M], const uint32_t (&inIy)[M],
@@ -278,7 +286,7 @@ __device__ __forceinline__ void cell_messages(
     const uint32_t s2ac = pk_mad(eac, pa.dm, pa.mm);
     const uint32_t s2bc = pk_mad(ebc, pa.dm, pa.mm);
     uint32_t s3;
-    if (pa.sop) s3 = pk_add(pk_add(s2ab, s2bc), s2ac);
+    if (SOPM < 0 ? pa.sop != 0 : SOPM == 1) s3 = pk_add(pk_add(s2ab, s2bc), s2ac);
     else s3 = pk_mad(eab, pk_mad(ebc, pa.s3_d1, pa.s3_d0), pa.s3_ne);
     const uint32_t sM = pk_add(inM[i], s3);
     const uint32_t sX = inIx[i], sY = inIy[i], sZ = inIz[i];
@@ -340,29 +348,29 @@ __device__ __forceinline__ uint32_t umin2(uint32_t a, uint32_t b) {
 }
 constexpr uint32_t SYM0 = 0x800u;  // helix symbol codes: SYM0 << s
 
-template <int M>
+// Terms that depend only on (b, c) are per-position constants for a whole row
+// (b changes when a position starts a new row at x = 1), kept in registers:
+//   SBC = dm*[b=c]                       (f16) added to the Iyz input
+//   K   = RTL: 2^13 (d0 + d1*[b=c])      fma multiplier of [a=b] for M
+//         SOP: 3 mismatch + dm*[b=c]     added to the M input
+template <int M, bool SOP>
 __device__ __forceinline__ void cell_messages_f16(
-    const uint32_t (&a)[M], const uint32_t (&b)[M], const uint32_t (&c)[M], uint32_t Q,
-    const PencilArgs &pa, const uint32_t (&inIx)[M], const uint32_t (&inIy)[M],
-    const uint32_t (&inIz)[M], const uint32_t (&inIxy)[M], const uint32_t (&inIyz)[M],
-    const uint32_t (&inIxz)[M], const uint32_t (&inM)[M], uint32_t (&nIx)[M], uint32_t (&oIy)[M],
-    uint32_t (&oIz)[M], uint32_t (&oIxy)[M], uint32_t (&oIyz)[M], uint32_t (&oIxz)[M],
-    uint32_t (&oBest)[M]) {
+    const uint32_t (&a)[M], const uint32_t (&b)[M], const uint32_t (&c)[M],
+    const uint32_t (&SBC)[M], const uint32_t (&K)[M], uint32_t Q, const PencilArgs &pa,
+    const uint32_t (&inIx)[M], const uint32_t (&inIy)[M], const uint32_t (&inIz)[M],
+    const uint32_t (&inIxy)[M], const uint32_t (&inIyz)[M], const uint32_t (&inIxz)[M],
+    const uint32_t (&inM)[M], uint32_t (&nIx)[M], uint32_t (&oIy)[M], uint32_t (&oIz)[M],
+    uint32_t (&oIxy)[M], uint32_t (&oIyz)[M], uint32_t (&oIxz)[M], uint32_t (&oBest)[M]) {
   const h2 DM = H(pa.h_dm), E = H(pa.E), O = H(pa.O), E2 = H(pa.E2), OE = H(pa.OE), O2 = H(pa.O2);
 #pragma unroll
   for (int i = 0; i < M; ++i) {
-    const uint32_t ab = a[i] & b[i];
-    const h2 eab = H(umin2(ab, Q)), eac = H(umin2(a[i] & c[i], Q)), ebc = H(umin2(b[i] & c[i], Q));
+    const h2 eab = H(umin2(a[i] & b[i], Q)), eac = H(umin2(a[i] & c[i], Q));
     const h2 sXY = hfma(eab, DM, H(inIxy[i]));  // src/PE_1cyc.v:159-161 (+mismatch folded)
-    const h2 sYZ = hfma(ebc, DM, H(inIyz[i]));
     const h2 sXZ = hfma(eac, DM, H(inIxz[i]));
+    const h2 sYZ = H(inIyz[i]) + H(SBC[i]);
     h2 sM;                                       // src/PE_1cyc.v:162
-    if (pa.sop) {
-      sM = hfma(eab, DM, hfma(ebc, DM, hfma(eac, DM, H(inM[i])))) + H(pa.h_c3);
-    } else {  // RTL: ne + eab*(d0 + ebc*d1) = ne + d0*[a=b] + d1*[a=b=c]
-      const h2 e3 = H(umin2(ab & c[i], Q));
-      sM = hfma(e3, H(pa.h_d1), hfma(eab, H(pa.h_d0), H(inM[i]))) + H(pa.h_c3);
-    }
+    if constexpr (SOP) sM = hfma(eab, DM, hfma(eac, DM, H(inM[i]))) + H(K[i]);
+    else sM = hfma(eab, H(K[i]), H(inM[i])) + H(pa.h_c3);  // ne + [a=b](d0 + [b=c] d1)
     const h2 sX = H(inIx[i]), sY = H(inIy[i]), sZ = H(inIz[i]);
     const h2 pYZ = hmax(sY, sZ), pXZ = hmax(sX, sZ), pXY = hmax(sX, sY);
     const h2 A1 = hmax3(pYZ, sXY, sXZ);  // Ix  <- {Iy,Iz,Ixy,Ixz} at GO+GE
@@ -409,7 +417,7 @@ __device__ __forceinline__ void zshift(uint32_t (&v)[M], const uint32_t (&src)[M
 //        sB  [LB] u32              B code, both halves
 //        fin [M][64] u32           best of the final step (wave w_f)
 // F16 selects the exact-f16 arithmetic above, else the int16 form.
-template <int M, int NW, bool F16>
+template <int M, int NW, bool F16, bool SOP>
 __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restrict__ seqs,
                                                          const int64_t *__restrict__ offs,
                                                          int32_t n, int32_t P, int32_t R,
@@ -435,6 +443,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
   uint32_t ones = F16 ? 0x08000800u : 0x00010001u;  // f16: match indicator 2^-13
   asm volatile("" : "+v"(ones));                     // keep it in a VGPR (VOP3P operand)
   const PencilArgs pv = F16 ? pa : pin_score_consts(pa);
+  uint32_t fsv = pa.f_single, fpv = pa.f_pair;  // VGPR copies for v_bfi_b32 / v_pk_mad_u16
+  uint32_t sbcv = pa.h_sbc, kdv = pa.h_kd, k0v = pa.h_k0, one1 = 0x00010001u;
+  asm volatile("" : "+v"(fsv), "+v"(fpv), "+v"(sbcv), "+v"(kdv), "+v"(k0v), "+v"(one1));
   // a[i] of this lane at step t is sA2[(t-w) mod P + 256 - lane - 128 i]
   const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
                           4u * (uint32_t)(256 - lane - 128 * (M - 1));
@@ -463,7 +474,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     __syncthreads();
 
     // ---- per-position registers (arrays [2] alternate roles between even/odd steps)
-    uint32_t b[M], c[M];
+    uint32_t b[M], c[M], SBC[M], K[M];
     uint32_t oIx[M], shIz[M], svIxy[M], svIyz[M], shIxz[2][M], svM[2][M];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
@@ -471,7 +482,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       const uint32_t c0 = k0 < lc ? SYM0 << (seqs[o2 + k0] & 3) : 0u;
       const uint32_t c1 = k1 < lc ? SYM0 << (seqs[o2 + k1] & 3) : 0u;
       c[i] = c0 | (c1 << 16);
-      b[i] = 0;  // set when a position reaches x = 1 of its lap
+      b[i] = SBC[i] = K[i] = 0;  // set when a position reaches x = 1 of its lap
       oIx[i] = pa.f_single;
       shIz[i] = pa.f_single;
       shIxz[0][i] = shIxz[1][i] = pa.f_pair;
@@ -481,6 +492,12 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     // position-0 bookkeeping (wave-uniform): u0 = t - w
     int32_t xpos0 = (P - (w % P)) % P;  // (t - w) mod P at t = 0
     int32_t lap0 = w == 0 ? 0 : -1;     // floor((t - w) / P)
+    // B code of row lap0*NW+w+1, taken by the position at x = 1 (0 past LB)
+    auto b_of_lap = [&](int32_t lp) -> uint32_t {
+      const int32_t r = lp * NW + w;
+      return (lp >= 0 && r < lb) ? sB[r] : 0u;
+    };
+    uint32_t binj = b_of_lap(lap0);
     const int32_t lap_f = (lb - 1) / NW, w_f = (lb - 1) % NW, k_f = lc - 1;
     const int32_t t_f = lap_f * P + (la - 1) + w_f + k_f;  // final cell (la, lb, lc)
     const int32_t T = t_f + 1;
@@ -500,9 +517,12 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     int32_t dma_row = ((PD - lag) % R + R) % R;  // ring row for step t + PD
     int32_t st_row = 0;                          // ring row written at step t (last wave)
 
-    // One step; PH = t & 1 picks the register roles and the LDS record slots.
-    auto step = [&](auto ph, int32_t t) {
+    // One step; PH = t & 1 picks the register roles and the LDS record slots,
+    // ROLE the wave's place in the lap (0: wave 0, reads the ring; 2: the last
+    // wave, writes it; 1: the others), so the loop body has no role branches.
+    auto step = [&](auto ph, auto role, int32_t t) {
       constexpr int PH = decltype(ph)::value;
+      constexpr int ROLE = decltype(role)::value;
       // this step's A codes (LDS table) and the B code of position x = 1
       uint32_t a[M];
       {
@@ -512,11 +532,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
           a[i] = *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t)(
               va + 512u * (uint32_t)(M - 1 - i));
       }
-      const int32_t row0 = lap0 * NW + w;
-      const uint32_t binj = (lap0 >= 0 && row0 < lb) ? sB[row0] : 0u;
       // ---- receive the wave-above record of step t-1
       uint4 rec[M];
-      if (w == 0) {
+      if constexpr (ROLE == 0) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(M * (PD - 1)) : "memory");
         const uint8_t *src = xr0 + (t % PD) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
@@ -547,22 +565,32 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll
         for (int i = 0; i < M; ++i) {
           if (i == is) {
-            inIx[i] = bfi(m1, pa.f_single, inIx[i]);
-            inIxy[i] = bfi(m1, pa.f_pair, inIxy[i]);
-            inIxz[i] = bfi(m1, pa.f_pair, inIxz[i]);
-            inM[i] = bfi(m1, 0u, inM[i]);
-            b[i] = bfi(m1, binj, b[i]);
+            inIx[i] = vbfi(m1, fsv, inIx[i]);
+            inIxy[i] = vbfi(m1, fpv, inIxy[i]);
+            inIxz[i] = vbfi(m1, fpv, inIxz[i]);
+            inM[i] = vbfi(m1, 0u, inM[i]);
+            b[i] = vbfi(m1, binj, b[i]);
+            if constexpr (F16) {  // re-derive the pair's per-row terms from the new b
+              const uint32_t e01 = pk_eq1(b[i], c[i], one1);
+              SBC[i] = pk_mad(e01, sbcv, 0u);
+              K[i] = pk_mad(e01, kdv, k0v);
+            }
           }
         }
       }
       uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
+      // Priority 0 for the cell arithmetic, 1 for the send/shift/barrier tail:
+      // VALU issue goes by priority then age, so without this the oldest waves
+      // of a SIMD finish each step first and idle at the barrier (+3-4 %).
+      __builtin_amdgcn_s_setprio(0);
       if constexpr (F16)
-        cell_messages_f16<M>(a, b, c, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx,
+        cell_messages_f16<M, SOP>(a, b, c, SBC, K, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx,
                              oIy, oIz, oIxy, oIyz, oIxz, oBest);
       else
-        cell_messages<M>(a, b, c, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx, oIy,
-                         oIz, oIxy, oIyz, oIxz, oBest);
+        cell_messages<M, SOP ? 1 : 0>(a, b, c, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz,
+                                      inM, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
 
+      __builtin_amdgcn_s_setprio(1);
       // ---- the final cell (src/TriAlign_1cyc.v:141-142,342-345) is in wave w_f's
       // last step; it is read back after the loop
       if (t == T - 1 && w == w_f) {
@@ -571,7 +599,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       }
 
       // ---- send this step's record to the wave below (or the ring)
-      if (w < NW - 1) {
+      if constexpr (ROLE != 2) {
         uint8_t *dst = xr + (w * 2 + PH) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
         for (int i = 0; i < M; ++i)
@@ -610,30 +638,38 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       zshift<M>(svIyz, rz, sel, mask0, pa.f_pair);
       zshift<M>(svM[PH], rw, sel, mask0, 0u);
       // position 0 advances to u0 + 1
-      if (++xpos0 == P) { xpos0 = 0; ++lap0; }
+      if (++xpos0 == P) {
+        xpos0 = 0;
+        binj = b_of_lap(++lap0);
+      }
 
       // ---- wave 0: fetch the record of step t + PD into the slot just consumed
-      if (w == 0) {
+      if constexpr (ROLE == 0) {
 #pragma unroll
         for (int i = 0; i < M; ++i)
           dma16(ring + ((int64_t)dma_row * M + i) * PAIR_BYTES + lane * REC_BYTES,
                 xr0 + (t % PD) * SLOT_BYTES + i * PAIR_BYTES);
         if (++dma_row == R) dma_row = 0;
       }
-      if (w == NW - 1) {
+      if constexpr (ROLE == 2) {
         if (++st_row == R) st_row = 0;
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(M * STORE_SLACK) : "memory");
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     };
 
-    int32_t t = 0;
+    auto run = [&](auto role) {
+      int32_t t = 0;
 #pragma unroll 1
-    for (; t + 1 < T; t += 2) {
-      step(std::integral_constant<int, 0>{}, t);
-      step(std::integral_constant<int, 1>{}, t + 1);
-    }
-    if (t < T) step(std::integral_constant<int, 0>{}, t);
+      for (; t + 1 < T; t += 2) {
+        step(std::integral_constant<int, 0>{}, role, t);
+        step(std::integral_constant<int, 1>{}, role, t + 1);
+      }
+      if (t < T) step(std::integral_constant<int, 0>{}, role, t);
+    };
+    if (w == 0) run(std::integral_constant<int, 0>{});
+    else if (w == NW - 1) run(std::integral_constant<int, 2>{});
+    else run(std::integral_constant<int, 1>{});
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -895,10 +931,14 @@ static PencilArgs make_args(const KParams &kp, bool f16) {
   a.O2 = pkh(2 * GO);
   a.f_single = pkh(fs);
   a.f_pair = pkh(fp + mm);
-  a.h_dm = pkh((kp.match - mm) * 8192.0);
-  a.h_d0 = pkh((kp.s3_ab - kp.s3_ne) * 8192.0);
-  a.h_d1 = pkh((kp.s3_eq - kp.s3_ab) * 8192.0);
-  a.h_c3 = pkh(a.sop ? 3.0 * mm : (double)kp.s3_ne);
+  const int32_t dm = kp.match - mm, d0 = kp.s3_ab - kp.s3_ne, d1 = kp.s3_eq - kp.s3_ab;
+  a.h_dm = pkh(dm * 8192.0);
+  a.h_c3 = pkh((double)kp.s3_ne);
+  a.h_sbc = pkh((double)dm);  // SBC = e01 * bits(dm), e01 in {0, 1}
+  const uint32_t k0 = a.sop ? pkh(3.0 * mm) : pkh(d0 * 8192.0);
+  const uint32_t k1 = a.sop ? pkh(3.0 * mm + dm) : pkh((d0 + d1) * 8192.0);
+  a.h_k0 = k0;                // K = k0 + e01 * (k1 - k0), per 16-bit half
+  a.h_kd = (((k1 & 0xFFFF) - (k0 & 0xFFFF)) & 0xFFFF) * 0x00010001u;
   return a;
 }
 
@@ -911,25 +951,27 @@ static bool use_f16(const KParams &kp, const Range &r) {
   auto fits = [](int64_t v) { return v >= -2048 && v <= 2048; };
   return r.lo - PENCIL_MARGIN >= -2048 && r.hi + PENCIL_MARGIN <= 2048 &&
          small((int64_t)kp.match - kp.mismatch) && small((int64_t)kp.s3_ab - kp.s3_ne) &&
-         small((int64_t)kp.s3_eq - kp.s3_ab) && fits(kp.mismatch) && fits(kp.s3_ne) &&
+         small((int64_t)kp.s3_eq - kp.s3_ab) && small((int64_t)kp.s3_eq - kp.s3_ne) &&
+         fits(kp.mismatch) && fits(kp.s3_ne) &&
          fits(3LL * kp.mismatch);
 }
 
-template <int M, int NW, bool F16>
+template <int M, int NW, bool F16, bool SOP>
 static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                     int32_t max_lb, const PencilGeom &g, int32_t *d_scores, void *d_ws,
                     const PencilArgs &pa, hipStream_t stream) {
   const int32_t lds_a = 4 * (g.P + 256), lds_b = 4 * ((max_lb + 3) & ~3);
   const size_t lds = (size_t)(NW - 1) * 2 * M * 1024 + (size_t)PD * M * 1024 + lds_a + lds_b +
                      (size_t)M * 64 * 4;
-  auto kfn = pencil_kernel<M, NW, F16>;
+  auto kfn = pencil_kernel<M, NW, F16, SOP>;
   if (lds > 160 * 1024) return TSA_EINVAL;
   if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return TSA_EDEVICE;
   const int grid = n < 65535 ? n : 65535;
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * NW), lds, stream, d_seqs, d_offsets, n, g.P,
-                     g.R, lds_a, lds_b, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, pa);
+                     g.R, lds_a, lds_b, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores,
+                     pa);
   return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
 }
 
@@ -973,12 +1015,18 @@ int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t
   const bool f16 = use_f16(kp, bound);
   const PencilArgs pa = make_args(kp, f16);
   int nw = PENCIL_NW_DEFAULT;
-  if (const char *e = getenv("TSA_PENCIL_NW")) nw = atoi(e) == 8 ? 8 : 16;  // tuning knob
-#define TSA_HELIX(MM, NN, FF) \
-  launch_m<MM, NN, FF>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_ws, pa, stream)
-#define TSA_HELIX_F(MM, NN) (f16 ? TSA_HELIX(MM, NN, true) : TSA_HELIX(MM, NN, false))
-  if (g.M == 1) return nw == 8 ? TSA_HELIX_F(1, 8) : TSA_HELIX_F(1, 16);
-  return nw == 8 ? TSA_HELIX_F(2, 8) : TSA_HELIX_F(2, 16);
+  if (const char *e = getenv("TSA_PENCIL_NW")) {  // tuning knob
+    const int v = atoi(e);
+    nw = (v == 4 || v == 8) ? v : 16;
+  }
+#define TSA_HELIX(MM, NN, FF, SS) \
+  launch_m<MM, NN, FF, SS>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_ws, pa, stream)
+#define TSA_HELIX_F(MM, NN)                                                           \
+  (f16 ? (pa.sop ? TSA_HELIX(MM, NN, true, true) : TSA_HELIX(MM, NN, true, false))   \
+       : (pa.sop ? TSA_HELIX(MM, NN, false, true) : TSA_HELIX(MM, NN, false, false)))
+  if (g.M == 1)
+    return nw == 4 ? TSA_HELIX_F(1, 4) : nw == 8 ? TSA_HELIX_F(1, 8) : TSA_HELIX_F(1, 16);
+  return nw == 4 ? TSA_HELIX_F(2, 4) : nw == 8 ? TSA_HELIX_F(2, 8) : TSA_HELIX_F(2, 16);
 #undef TSA_HELIX_F
 #undef TSA_HELIX
 }

@@ -149,6 +149,41 @@ def test_pencil_waves_per_workgroup(gpu, orc, monkeypatch, nw):
         assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (nw, la, lb, lc)
 
 
+@pytest.mark.parametrize("arith", ["f16", "i16"])
+@pytest.mark.parametrize("s3_mode", [0, 1])
+def test_pencil_arithmetic_forms(gpu, orc, monkeypatch, arith, s3_mode):
+    # helix kernel: exact-f16 (default where the value bound allows) and int16
+    # message arithmetic, RTL and sum-of-pairs triple scores, several penalty sets
+    monkeypatch.setenv("TSA_PENCIL_MODE", "helix")
+    monkeypatch.setenv("TSA_PENCIL_ARITH", arith)
+    rng = np.random.default_rng(40 + s3_mode)
+    for kw in [dict(), dict(match=2, mismatch=-3, gap_open=5, gap_extend=2),
+               dict(match=1, mismatch=0, gap_open=3, gap_extend=1),
+               dict(match=3, mismatch=-1, gap_open=2, gap_extend=2, score_bits=16)]:
+        kw = dict(kw, s3_mode=s3_mode)
+        p, op = gpu.TsaParams.default(**kw), orc.default_params(**kw)
+        for la, lb, lc in [(256, 24, 256), (90, 41, 100), (130, 9, 255)]:
+            a, b, c = (rng.integers(0, 4, n).astype(np.uint8) for n in (la, lb, lc))
+            if rng.random() < 0.5:  # related sequences: long matching runs
+                b[: min(la, lb)] = a[: min(la, lb)]
+            try:
+                got = gpu.score(a, b, c, p, kernel="pencil")
+            except gpu.TsaError:
+                continue  # pencil not exact for this bound: AUTO would use plane
+            assert got == orc.score(a, b, c, op), (arith, kw, la, lb, lc)
+
+
+def test_pencil_int16_when_f16_range_exceeded(gpu, orc):
+    # |values| > 2048: the host must fall back to the int16 form (score_bits 16)
+    rng = np.random.default_rng(77)
+    p, op = gpu.TsaParams.default(match=5, score_bits=16), orc.default_params(match=5, score_bits=16)
+    a = rng.integers(0, 4, 256).astype(np.uint8)
+    c = a.copy()
+    c[::17] = (c[::17] + 1) % 4
+    b = a[:200].copy()
+    assert gpu.score(a, b, c, p, kernel="pencil") == orc.score(a, b, c, op)
+
+
 @pytest.mark.parametrize("mode", ["helix", "lap"])
 def test_pencil_single_cube_modes(gpu, orc, synth, monkeypatch, mode):
     # "lap": one 16-row lap per workgroup, laps chained through global memory
