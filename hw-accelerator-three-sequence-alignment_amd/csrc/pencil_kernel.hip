@@ -132,11 +132,13 @@ static bool use_lap_mode(int32_t n, int32_t max_lb) {
 
 size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
   if (!pencil_shape_ok(max_la, max_lb, max_lc)) return 0;
-  if (use_lap_mode(n, max_lb)) {
+  const size_t helix = (size_t)std::min<int32_t>(n, 65535) *
+                       (size_t)pencil_geom(max_la, max_lc).ring_bytes_per_triple;
+  if (use_lap_mode(n, max_lb)) {  // the lap kernel unless the params need int16
     const LapGeom g = lap_geom(n, max_la, max_lb, max_lc);
-    return g.flag_bytes + g.yf_bytes;
+    return std::max(helix, g.flag_bytes + g.yf_bytes);
   }
-  return (size_t)n * (size_t)pencil_geom(max_la, max_lc).ring_bytes_per_triple;
+  return helix;
 }
 
 bool pencil_shape_supported(int32_t max_la, int32_t max_lb, int32_t max_lc) {
@@ -228,42 +230,6 @@ __device__ __forceinline__ void lds_write16(uint8_t *p, uint4 v) {
 __device__ __forceinline__ uint32_t ror1(uint32_t v) {  // lane l <- lane l-1, lane 0 <- lane 63
   // mov_dpp (old = undef): wave_ror:1 reads a valid lane for every lane
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xF, 0xF, false);
-}
-
-// Shift a packed per-position value one position up the helix (k <- k-1):
-// lanes >= 1 take lane-1's pair as is; lane 0 takes (pair i-1).hi and
-// (pair i).lo of lane 63; position 0 (lane 0, pair 0, lo) gets `inj`.
-template <int M>
-__device__ __forceinline__ void shift_pos(uint32_t (&v)[M], uint32_t sel, uint32_t mask0,
-                                          uint32_t inj) {
-  uint32_t r[M];
-#pragma unroll
-  for (int i = 0; i < M; ++i) r[i] = ror1(v[i]);
-#pragma unroll
-  for (int i = 0; i < M; ++i) v[i] = __builtin_amdgcn_perm(r[i], r[(i + M - 1) % M], sel);
-  v[0] = bfi(mask0, inj, v[0]);
-}
-
-// The x == 1 position k* (if inside this lane span) takes the x = 0 face for
-// its x-1 inputs (EN_i==1&&EN==0 gating, src/PE_1cyc.v:164-178,196-202,212-218).
-template <int M>
-__device__ __forceinline__ void x1_substitute(int ks, int lane, const PencilArgs &pa,
-                                              uint32_t (&inIx)[M], uint32_t (&inIxy)[M],
-                                              uint32_t (&inIxz)[M], uint32_t (&inM)[M]) {
-  if (ks >= 0 && ks < 128 * M) {
-    const uint32_t hm = (ks >> 6) & 1 ? 0xFFFF0000u : 0x0000FFFFu;
-    const uint32_t m1 = lane == (ks & 63) ? hm : 0u;
-    const int is = ks >> 7;
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      if (i == is) {
-        inIx[i] = bfi(m1, pa.f_single, inIx[i]);
-        inIxy[i] = bfi(m1, pa.f_pair, inIxy[i]);
-        inIxz[i] = bfi(m1, pa.f_pair, inIxz[i]);
-        inM[i] = bfi(m1, 0u, inM[i]);
-      }
-    }
-  }
 }
 
 // One step of M packed cell pairs: scores (src/PE_1cyc.v:159-162) on one-hot
@@ -683,43 +649,47 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 }
 
 // ---------------------------------------------------------------------------
-// Single-cube variant: one 16-row lap per workgroup, all laps of a triple in
+// Single-cube variant: one NW-row lap per workgroup, all laps of a triple in
 // flight at once (blockIdx.x = tri * G + L). Lap L's last wave hands its
 // per-step record rows down to lap L+1's wave 0 through global memory:
 //   producer: write-through (sc1) row stores; each step a counted vmcnt proves
 //             rows <= tau-STORE_SLACK complete, then one agent-scope flag store
 //             publishes that count (MI355X_MICROARCH.md "Valid forms", row 1);
-//   consumer: before LDS-DMA'ing (sc1) a row it has not yet seen published, it
-//             drains its own queue and polls the flag with agent-scope loads.
+//   consumer: the flag word travels with the rows (LDS-DMA, LPD steps ahead);
+//             only when it does not yet cover a row does wave 0 drain its
+//             queue and poll the flag with agent-scope loads.
 // Every workgroup of the grid must be resident (host: n*G <= resident WGs), so
 // a spinning consumer never blocks its producer. Spins are bounded: on
 // timeout the kernel sets *err and carries on (scores then invalid).
+// Cell arithmetic, registers and shifts are the helix kernel's (exact f16);
+// each wave owns one row, so B and the per-row score terms are constants.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void store16_sc1(void *gptr, uint4 v) {
   const u32x4 d = {v.x, v.y, v.z, v.w};
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(gptr), "v"(d) : "memory");
 }
 
-template <int M, int NW>
+template <int M, int NW, bool SOP>
 __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     const uint8_t *__restrict__ seqs, const int64_t *__restrict__ offs, int32_t G, int32_t YR,
-    uint8_t *__restrict__ yf_base, int32_t *__restrict__ flags, int32_t *__restrict__ err,
-    int32_t *__restrict__ scores, PencilArgs pa) {
+    int32_t lds_a, uint8_t *__restrict__ yf_base, int32_t *__restrict__ flags,
+    int32_t *__restrict__ err, int32_t *__restrict__ scores, PencilArgs pa) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int PAIR_BYTES = 64 * REC_BYTES;
   constexpr int SLOT_BYTES = M * PAIR_BYTES;
-  uint8_t *xr = smem;                             // [NW-1][2][M][64][16]
-  uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT_BYTES;  // [LPD][M][64][16]
+  constexpr int ZT = 128 * M;
+  uint8_t *xr = smem;                                    // [NW-1][2][M][64][16]
+  uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT_BYTES;         // [LPD][M][64][16]
   int32_t *fslot = (int32_t *)(xr0 + LPD * SLOT_BYTES);  // [LPD] prefetched producer flags
-  uint8_t *sA = (uint8_t *)(fslot + LPD);          // one-hot A
+  uint32_t *fin = (uint32_t *)(fslot + LPD);             // [M][64] final-step best
+  uint32_t *sA2 = fin + M * 64;                          // [la + lc + NW + 256] A code pairs
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t sel = lane == 0 ? 0x05040302u : 0x07060504u;
   const uint32_t mask0 = lane == 0 ? 0x0000FFFFu : 0u;
-  uint32_t ones = 0x00010001u;
-  asm volatile("" : "+v"(ones));
-  const PencilArgs pv = pin_score_consts(pa);
+  uint32_t Q = 0x08000800u, fsv = pa.f_single, fpv = pa.f_pair;
+  asm volatile("" : "+v"(Q), "+v"(fsv), "+v"(fpv));
 
   const int32_t tri = blockIdx.x / G, L = blockIdx.x % G;
   const int64_t o0 = offs[3 * (int64_t)tri], o1 = offs[3 * (int64_t)tri + 1];
@@ -727,42 +697,55 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
   const int32_t la = (int32_t)(o1 - o0), lb = (int32_t)(o2 - o1), lc = (int32_t)(o3 - o2);
   const int32_t nlap = (lb + NW - 1) / NW;
   if (L >= nlap) return;  // whole workgroup
-  const int32_t T = la + (NW - 1) + (lc - 1);      // steps of this lap
+  const bool final_lap = L == nlap - 1;
+  const int32_t w_f = (lb - 1) % NW, k_f = lc - 1;
+  // steps of this lap; the final lap stops at the final cell (la, lb, lc)
+  const int32_t T = final_lap ? (la - 1) + w_f + k_f + 1 : la + (NW - 1) + (lc - 1);
   uint8_t *yf_mine = yf_base + ((int64_t)tri * G + L) * YR * SLOT_BYTES;
   const uint8_t *yf_prev = yf_mine - (int64_t)YR * SLOT_BYTES;
   int32_t *flag_mine = flags + (int64_t)tri * G + L;
   const int32_t *flag_prev = flag_mine - 1;
 
-  for (int i = threadIdx.x; i < la; i += 64 * NW) sA[i] = (uint8_t)(1u << (seqs[o0 + i] & 3));
-  __syncthreads();
-
-  const int32_t y = L * NW + w + 1;                 // this wave's DP row
-  const uint32_t bw = y <= lb ? (1u << (seqs[o1 + y - 1] & 3)) * 0x00010001u : 0u;
-  uint32_t a[M], b[M], c[M];
-  uint32_t oIx[M], shIz[M], shIxz1[M], shIxz2[M], svIxy[M], svIyz[M], svM1[M], svM2[M];
-#pragma unroll
-  for (int i = 0; i < M; ++i) {
-    const int k0 = lane + 128 * i, k1 = lane + 64 + 128 * i;
-    const uint32_t c0 = k0 < lc ? 1u << (seqs[o2 + k0] & 3) : 0u;
-    const uint32_t c1 = k1 < lc ? 1u << (seqs[o2 + k1] & 3) : 0u;
-    c[i] = c0 | (c1 << 16);
-    b[i] = bw;  // one row per wave: B is constant
-    a[i] = (i == 0 && w == 0 && lane == 0) ? (uint32_t)sA[0] : 0u;  // only (x=1,k=0) started
-    oIx[i] = pa.f_single;
-    shIz[i] = pa.f_single;
-    shIxz1[i] = shIxz2[i] = pa.f_pair;
-    svIxy[i] = svIyz[i] = pa.f_pair;
-    svM1[i] = svM2[i] = 0;
+  // A code pairs: entry j holds x = j-256 (lo) and x = j-320 (hi), 0 outside [0, la)
+  const int32_t na = lds_a / 4;
+  for (int j = threadIdx.x; j < na; j += 64 * NW) {
+    const int x0 = j - 256, x1 = j - 320;
+    const uint32_t c0 = (x0 >= 0 && x0 < la) ? SYM0 << (seqs[o0 + x0] & 3) : 0u;
+    const uint32_t c1 = (x1 >= 0 && x1 < la) ? SYM0 << (seqs[o0 + x1] & 3) : 0u;
+    sA2[j] = c0 | (c1 << 16);
   }
-  const int32_t w_f = (lb - 1) % NW, k_f = lc - 1;
-  const bool final_lap = L == (lb - 1) / NW;
-  const int32_t t_f = (la - 1) + w_f + k_f;
-  const int32_t l_f = k_f & 63, i_f = k_f >> 7, h_f = (k_f >> 6) & 1;
+  __syncthreads();
+  // position k of this wave is at x-1 = t - w - k: a[i] = sA2[t - w + 256 - lane - 128 i]
+  const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
+                          4u * (uint32_t)(256 - w - lane - 128 * (M - 1));
+
+  const int32_t y = L * NW + w + 1;  // this wave's DP row
+  const uint32_t bw = y <= lb ? (SYM0 << (seqs[o1 + y - 1] & 3)) * 0x00010001u : 0u;
+  uint32_t b[M], c[M], SBC[M], K[M];
+  uint32_t oIx[M], shIz[M], svIxy[M], svIyz[M], shIxz[2][M], svM[2][M];
+  {
+    uint32_t one1 = 0x00010001u, sbcv = pa.h_sbc, kdv = pa.h_kd, k0v = pa.h_k0;
+    asm volatile("" : "+v"(one1), "+v"(sbcv), "+v"(kdv), "+v"(k0v));
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const int k0 = lane + 128 * i, k1 = lane + 64 + 128 * i;
+      const uint32_t c0 = k0 < lc ? SYM0 << (seqs[o2 + k0] & 3) : 0u;
+      const uint32_t c1 = k1 < lc ? SYM0 << (seqs[o2 + k1] & 3) : 0u;
+      c[i] = c0 | (c1 << 16);
+      b[i] = bw;  // one row per wave
+      const uint32_t e01 = pk_eq1(bw, c[i], one1);
+      SBC[i] = pk_mad(e01, sbcv, 0u);
+      K[i] = pk_mad(e01, kdv, k0v);
+      oIx[i] = shIz[i] = pa.f_single;
+      shIxz[0][i] = shIxz[1][i] = svIxy[i] = svIyz[i] = pa.f_pair;
+      svM[0][i] = svM[1][i] = 0;
+    }
+  }
 
   // wave 0 of lap L>0: row r of yf_prev feeds step r - (NW-1); prime LPD steps
   int32_t seen = 0;  // rows of yf_prev known complete
-  auto ensure = [&](int32_t r) {  // r < T: row r must be published
-    if (r < seen || r >= T) return;
+  auto ensure = [&](int32_t r) {  // row r must be published (r < the producer's T)
+    if (r < seen) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (uint32_t spin = 0;; ++spin) {
       seen = __builtin_amdgcn_readfirstlane(
@@ -770,43 +753,54 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
       if (r < seen) break;
       if (spin > (1u << 22)) {
         if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        seen = T;
+        seen = 1 << 30;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
   };
-  if (w == 0 && L > 0) {
-    for (int s2 = 0; s2 < LPD; ++s2) {
-      const int32_t r = s2 + NW - 1;
-      ensure(r);
+  const int32_t T_prev = la + (NW - 1) + (lc - 1);  // rows lap L-1 publishes
+  auto fetch = [&](int32_t s2) {  // rows of step s2 -> xr0 slot s2 % LPD
+    const int32_t r = s2 + NW - 1;
+    if (r < T_prev) ensure(r);
+    const int32_t rr = r < T_prev ? r : T_prev - 1;  // past the end: any valid row
 #pragma unroll
-      for (int i = 0; i < M; ++i)
-        dma16(yf_prev + ((int64_t)r * M + i) * PAIR_BYTES + lane * REC_BYTES,
-              xr0 + (s2 % LPD) * SLOT_BYTES + i * PAIR_BYTES);
-      if (lane == 0) dma4(flag_prev, fslot + (s2 % LPD));
-    }
-  }
+    for (int i = 0; i < M; ++i)
+      dma16(yf_prev + ((int64_t)rr * M + i) * PAIR_BYTES + lane * REC_BYTES,
+            xr0 + (s2 % LPD) * SLOT_BYTES + i * PAIR_BYTES);
+    if (lane == 0) dma4(flag_prev, fslot + (s2 % LPD));
+  };
+  if (w == 0 && L > 0)
+    for (int s2 = 0; s2 < LPD; ++s2) fetch(s2);
   const uint4 face = make_uint4(pa.f_single, pa.f_pair, pa.f_pair, 0u);
 
-#pragma unroll 1
-  for (int32_t t = 0; t < T; ++t) {
+  // ROLE 0: wave 0 of lap 0 (y = 0 face above); 1: wave 0 of a later lap (rows
+  // of lap L-1 via LDS-DMA); 2: middle waves; 3: the last wave (rows to global)
+  auto step = [&](auto ph, auto role, int32_t t) {
+    constexpr int PH = decltype(ph)::value;
+    constexpr int ROLE = decltype(role)::value;
+    uint32_t a[M];
+    {
+      const uint32_t va = a_lane + 4u * (uint32_t)t;
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+        a[i] = *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t)(
+            va + 512u * (uint32_t)(M - 1 - i));
+    }
     uint4 rec[M];
-    if (w == 0) {
-      if (L == 0) {
+    if constexpr (ROLE == 0) {
 #pragma unroll
-        for (int i = 0; i < M; ++i) rec[i] = face;  // y = 0 face
-      } else {
-        // rows + flag of step t were DMA'd LPD steps ago: M+1 ops per step
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((M + 1) * (LPD - 1)) : "memory");
-        const uint8_t *src = xr0 + (t % LPD) * SLOT_BYTES + lane * REC_BYTES;
+      for (int i = 0; i < M; ++i) rec[i] = face;
+    } else if constexpr (ROLE == 1) {
+      // rows + flag of step t were DMA'd LPD steps ago: M+1 ops per step
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((M + 1) * (LPD - 1)) : "memory");
+      const uint8_t *src = xr0 + (t % LPD) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
-        for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
-        // producer progress as of ~LPD steps ago, free of any round trip
-        seen = max(seen, __builtin_amdgcn_readfirstlane(fslot[t % LPD]));
-      }
+      for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
+      // producer progress as of ~LPD steps ago, free of any round trip
+      seen = max(seen, __builtin_amdgcn_readfirstlane(fslot[t % LPD]));
     } else {
-      const uint8_t *src = xr + ((w - 1) * 2 + ((t - 1) & 1)) * SLOT_BYTES + lane * REC_BYTES;
+      const uint8_t *src = xr + ((w - 1) * 2 + (PH ^ 1)) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
       for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
     }
@@ -818,16 +812,36 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
       inIz[i] = shIz[i];
       inIxy[i] = svIxy[i];
       inIyz[i] = svIyz[i];
-      inIxz[i] = shIxz2[i];
-      inM[i] = svM2[i];
+      inIxz[i] = shIxz[PH][i];
+      inM[i] = svM[PH][i];
     }
-    x1_substitute<M>(t - w, lane, pa, inIx, inIxy, inIxz, inM);
+    // x == 1 at position k* = t - w: x = 0 face inputs (src/PE_1cyc.v:164-178,196-218)
+    const int32_t ks = t - w;
+    if (ks >= 0 && ks < ZT) {
+      const uint32_t hm = (ks >> 6) & 1 ? 0xFFFF0000u : 0x0000FFFFu;
+      const uint32_t m1 = lane == (ks & 63) ? hm : 0u;
+      const int is = ks >> 7;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        if (i == is) {
+          inIx[i] = vbfi(m1, fsv, inIx[i]);
+          inIxy[i] = vbfi(m1, fpv, inIxy[i]);
+          inIxz[i] = vbfi(m1, fpv, inIxz[i]);
+          inM[i] = vbfi(m1, 0u, inM[i]);
+        }
+      }
+    }
     uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
-    cell_messages<M>(a, b, c, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx, oIy, oIz,
-                     oIxy, oIyz, oIxz, oBest);
-
-    if (w < NW - 1) {
-      uint8_t *dst = xr + (w * 2 + (t & 1)) * SLOT_BYTES + lane * REC_BYTES;
+    __builtin_amdgcn_s_setprio(0);
+    cell_messages_f16<M, SOP>(a, b, c, SBC, K, Q, pa, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM,
+                              nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
+    __builtin_amdgcn_s_setprio(1);
+    if (final_lap && t == T - 1 && w == w_f) {
+#pragma unroll
+      for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
+    }
+    if constexpr (ROLE != 3) {
+      uint8_t *dst = xr + (w * 2 + PH) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
       for (int i = 0; i < M; ++i)
         lds_write16(dst + i * PAIR_BYTES, make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
@@ -837,42 +851,20 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
         store16_sc1(yf_mine + ((int64_t)t * M + i) * PAIR_BYTES + lane * REC_BYTES,
                     make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
     }
-    if (final_lap && t == t_f && w == w_f) {
-      uint32_t v = oBest[0];
-#pragma unroll
-      for (int i = 1; i < M; ++i) if (i == i_f) v = oBest[i];
-      if (lane == l_f) scores[tri] = (int32_t)(int16_t)(h_f ? (v >> 16) : (v & 0xFFFF));
-    }
 #pragma unroll
     for (int i = 0; i < M; ++i) {
       oIx[i] = nIx[i];
-      shIxz2[i] = shIxz1[i];
-      shIxz1[i] = oIxz[i];
-      shIz[i] = oIz[i];
       svIxy[i] = rec[i].y;
-      svIyz[i] = rec[i].z;
-      svM2[i] = svM1[i];
-      svM1[i] = rec[i].w;
     }
-    shift_pos<M>(shIxz1, sel, mask0, pa.f_pair);
-    shift_pos<M>(shIz, sel, mask0, pa.f_single);
-    shift_pos<M>(svIyz, sel, mask0, pa.f_pair);
-    shift_pos<M>(svM1, sel, mask0, 0u);
-    {
-      const int32_t xi = t + 1 - w;  // position 0's x-1 at step t+1
-      const uint32_t ainj = (xi >= 0 && xi < la) ? (uint32_t)sA[xi] : 0u;
-      shift_pos<M>(a, sel, mask0, ainj);
-    }
-    if (w == 0 && L > 0) {
-      const int32_t r = t + LPD + NW - 1;  // row for step t + LPD
-      ensure(r);  // usually satisfied by the prefetched flag: no round trip
+    uint32_t rz[M], rw[M];
 #pragma unroll
-      for (int i = 0; i < M; ++i)
-        dma16(yf_prev + ((int64_t)r * M + i) * PAIR_BYTES + lane * REC_BYTES,
-              xr0 + (t % LPD) * SLOT_BYTES + i * PAIR_BYTES);
-      if (lane == 0) dma4(flag_prev, fslot + (t % LPD));
-    }
-    if (w == NW - 1) {
+    for (int i = 0; i < M; ++i) { rz[i] = rec[i].z; rw[i] = rec[i].w; }
+    zshift<M>(shIxz[PH], oIxz, sel, mask0, pa.f_pair);  // z = 0 face for position 0
+    zshift<M>(shIz, oIz, sel, mask0, pa.f_single);
+    zshift<M>(svIyz, rz, sel, mask0, pa.f_pair);
+    zshift<M>(svM[PH], rw, sel, mask0, 0u);
+    if constexpr (ROLE == 1) fetch(t + LPD);  // usually covered by the prefetched flag
+    if constexpr (ROLE == 3) {
       // rows <= t - STORE_SLACK complete (M stores + 1 flag store per step)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STORE_SLACK * (M + 1)) : "memory");
       // exactly M + 1 vector-memory ops per step keep that count exact
@@ -881,12 +873,38 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  auto run = [&](auto role) {
+    int32_t t = 0;
+#pragma unroll 1
+    for (; t + 1 < T; t += 2) {
+      step(std::integral_constant<int, 0>{}, role, t);
+      step(std::integral_constant<int, 1>{}, role, t + 1);
+    }
+    if (t < T) step(std::integral_constant<int, 0>{}, role, t);
+  };
+  if (w == 0) {
+    if (L == 0) run(std::integral_constant<int, 0>{});
+    else run(std::integral_constant<int, 1>{});
+  } else if (w == NW - 1) {
+    run(std::integral_constant<int, 3>{});
+  } else {
+    run(std::integral_constant<int, 2>{});
   }
   if (w == NW - 1) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) __hip_atomic_store(flag_mine, T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (final_lap) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int32_t l_f = k_f & 63, i_f = k_f >> 7, h_f = (k_f >> 6) & 1;
+      const uint32_t v = fin[i_f * 64 + l_f];
+      scores[tri] = (int32_t)(float)__builtin_bit_cast(
+          _Float16, (uint16_t)(h_f ? (v >> 16) : (v & 0xFFFF)));
+    }
+  }
 }
 
 
@@ -975,13 +993,15 @@ static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
   return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
 }
 
-template <int M, int NW>
+template <int M, int NW, bool SOP>
 static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, int32_t max_la,
-                      const LapGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
-                      hipStream_t stream) {
+                      int32_t max_lc, const LapGeom &g, int32_t *d_scores, void *d_ws,
+                      const PencilArgs &pa, hipStream_t stream) {
+  const int32_t lds_a = 4 * ((max_la + max_lc + NW + 256 + 3) & ~3);
   const size_t lds = (size_t)(NW - 1) * 2 * M * 1024 + (size_t)LPD * M * 1024 + LPD * 4 +
-                     ((max_la + 15) & ~15);
-  auto kfn = pencil_lap_kernel<M, NW>;
+                     (size_t)M * 64 * 4 + lds_a;
+  auto kfn = pencil_lap_kernel<M, NW, SOP>;
+  if (lds > 160 * 1024) return TSA_EINVAL;
   if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return TSA_EDEVICE;
@@ -989,7 +1009,7 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
   if (hipMemsetAsync(flags, 0, g.flag_bytes, stream) != hipSuccess) return TSA_EDEVICE;
   uint8_t *yf = (uint8_t *)d_ws + g.flag_bytes;
   hipLaunchKernelGGL(kfn, dim3(n * g.G), dim3(64 * NW), lds, stream, d_seqs, d_offsets, g.G, g.YR,
-                     yf, flags, flags + (size_t)n * g.G, d_scores, pa);
+                     lds_a, yf, flags, flags + (size_t)n * g.G, d_scores, pa);
   return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
 }
 
@@ -999,11 +1019,16 @@ int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t
                         hipStream_t stream) {
   if (n <= 0) return TSA_OK;
   if (!pencil_shape_ok(max_la, max_lb, max_lc)) return TSA_EINVAL;
-  if (use_lap_mode(n, max_lb)) {
+  const bool f16 = use_f16(kp, bound);
+  const PencilArgs pa = make_args(kp, f16);
+  if (f16 && use_lap_mode(n, max_lb)) {  // the lap kernel is f16-only; else helix
     const LapGeom lg = lap_geom(n, max_la, max_lb, max_lc);
     if (ws_bytes < lg.flag_bytes + lg.yf_bytes) return TSA_ENOMEM;
-    const PencilArgs pa = make_args(kp, false);
-#define TSA_LAP(MM, NN) launch_lap<MM, NN>(d_seqs, d_offsets, n, max_la, lg, d_scores, d_ws, pa, stream)
+#define TSA_LAP(MM, NN)                                                                    \
+  (pa.sop ? launch_lap<MM, NN, true>(d_seqs, d_offsets, n, max_la, max_lc, lg, d_scores, d_ws, \
+                                     pa, stream)                                           \
+          : launch_lap<MM, NN, false>(d_seqs, d_offsets, n, max_la, max_lc, lg, d_scores,   \
+                                      d_ws, pa, stream))
     if (pencil_pairs(max_lc) == 1)
       return lg.NW == 4 ? TSA_LAP(1, 4) : lg.NW == 8 ? TSA_LAP(1, 8) : TSA_LAP(1, 16);
     return lg.NW == 4 ? TSA_LAP(2, 4) : lg.NW == 8 ? TSA_LAP(2, 8) : TSA_LAP(2, 16);
@@ -1012,8 +1037,6 @@ int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t
   const PencilGeom g = pencil_geom(max_la, max_lc);
   const int32_t grid = n < 65535 ? n : 65535;
   if (ws_bytes < (size_t)grid * (size_t)g.ring_bytes_per_triple) return TSA_ENOMEM;
-  const bool f16 = use_f16(kp, bound);
-  const PencilArgs pa = make_args(kp, f16);
   int nw = PENCIL_NW_DEFAULT;
   if (const char *e = getenv("TSA_PENCIL_NW")) {  // tuning knob
     const int v = atoi(e);
