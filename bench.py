@@ -35,7 +35,9 @@ PKG_DIR = os.path.join(ROOT, "hw-accelerator-three-sequence-alignment_amd")
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 BYTES_PER_CELL = 28            # 7 int16 states written + read once
-VALU_LANE_OPS_PER_S = 256 * 4 * 32 * 2.4e9   # 256 CU x 4 SIMD32 x 2.4 GHz
+# VALU issue ceiling: 256 CU x 4 SIMD, one wave64 VALU instruction per 4 cycles
+# per SIMD (MI355X_MICROARCH.md "vector-instruction ISSUE cost"), 2.4 GHz
+VALU_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 4
 
 
 def log(*a):
@@ -51,18 +53,18 @@ def load_pkg():
     return mod
 
 
-def load_pmc_traffic(kernel_name: str, workload: str):
-    """HBM bytes per launch from the committed PMC pass (profiles/pmc_*.json,
-    written by tools/pmc_traffic.py per the MI355X_MICROARCH.md HBM recipe)."""
+def load_pmc(kernel_name: str, workload: str) -> dict:
+    """Per-launch PMC figures from the committed profile (profiles/pmc_*.json,
+    written by tools/pmc_traffic.py per the MI355X_MICROARCH.md HBM recipe):
+    hbm_bytes_per_launch (FETCH_SIZE x2 + WRITE_SIZE) and valu_insts_per_launch."""
     path = os.path.join(ROOT, "profiles", f"pmc_{kernel_name}_{workload}.json")
     if not os.path.exists(path):
-        return None
+        return {}
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get("hbm_bytes_per_launch")
+            return json.load(f)
     except Exception:  # noqa: BLE001
-        return None
+        return {}
 
 
 def main():
@@ -163,7 +165,19 @@ def main():
     # per-rank kernel time of THIS rank's stream (HIP events on the launch stream)
     per_gpu_cells = n * cells_per_triple
     achieved_gbs = per_gpu_cells * BYTES_PER_CELL / (kernel_ms_per_step * 1e-3) / 1e9
-    traffic = load_pmc_traffic(kernel_name, args.workload)
+    pmc = load_pmc(kernel_name, args.workload) if (L == 256 and per_gpu == 512) else {}
+    traffic = pmc.get("hbm_bytes_per_launch")
+    valu = None
+    if pmc.get("valu_insts_per_launch") and kind == "pencil":
+        # the binding resource of the pencil kernel: VALU issue (states never
+        # leave the chip, so the 28 B/cell streaming roofline is exceeded)
+        insts = pmc["valu_insts_per_launch"]
+        ach = insts / (kernel_ms_per_step * 1e-3)
+        valu = {"bound": "valu", "achieved": round(ach / 1e9, 2), "peak": VALU_WAVE_INSTR_PER_S / 1e9,
+                "unit": "G wave-instr/s", "frac": round(ach / VALU_WAVE_INSTR_PER_S, 4),
+                "insts_per_launch": insts,
+                "lane_insts_per_cell": round(insts * 64 / per_gpu_cells, 3),
+                "source": f"SQ_INSTS_VALU, profiles/pmc_{kernel_name}_{args.workload}.json"}
 
     # single-cube latency, configs[2]
     single = None
@@ -257,6 +271,8 @@ def main():
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
             "kernel": kernel_name, "bytes_per_cell": BYTES_PER_CELL,
             "kernel_ms_per_step": round(kernel_ms_per_step, 4),
+            "traffic_bytes_per_cell": (round(traffic / per_gpu_cells, 3) if traffic else None),
+            "valu": valu,
         },
         "cpu_baseline": cpu_baseline,
         "single_cube": single,

@@ -4,7 +4,8 @@
 For each kernel directory under gpurun_out/prof_<tag>/<kernel>/ this reads the
 rocprofv3 kernel trace (per-dispatch durations, grouped by grid size so the
 batch launch and the single-cube launch are separated) and the two PMC passes
-(FETCH_SIZE, WRITE_SIZE; separate runs as MI355X_MICROARCH.md prescribes) and
+(FETCH_SIZE, WRITE_SIZE; separate runs as MI355X_MICROARCH.md prescribes), the
+SQ_INSTS_VALU pass (wave-level VALU instructions per dispatch), and
 writes
   profiles/<tag>_<kernel>_kernel_stats.csv   (rocprofv3 --stats summary, copied)
   profiles/pmc_<kernel_name>_batch.json      (read by bench.py: traffic field)
@@ -52,7 +53,7 @@ def main(tag="r1"):
             per[key].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
             names[key] = name
         pmc = defaultdict(lambda: defaultdict(list))
-        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        for c in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"):
             p = os.path.join(d, f"pmc_{c}", "run_counter_collection.csv")
             if not os.path.exists(p):
                 continue
@@ -75,6 +76,8 @@ def main(tag="r1"):
                 if fk is not None and wk is not None:
                     ent["hbm_bytes_raw"] = (fk + wk) * 1024
                     ent["hbm_bytes_corrected"] = (2 * fk + wk) * 1024
+                if pmc[key]["SQ_INSTS_VALU"]:
+                    ent["valu_insts"] = statistics.mean(pmc[key]["SQ_INSTS_VALU"])
             ks[f"{kname}@{grid}"] = ent
         summary[kdir] = ks
         # bench.py traffic: the batch launch = the largest grid of the main kernel
@@ -88,6 +91,7 @@ def main(tag="r1"):
                     json.dump({"tag": tag, "kernel": big["kernel"], "grid_size": big["grid_size"],
                                "avg_ns": big["avg_ns"], "hbm_bytes_per_launch": big["hbm_bytes_corrected"],
                                "hbm_bytes_raw": big["hbm_bytes_raw"],
+                               "valu_insts_per_launch": big.get("valu_insts"),
                                "note": "(2*FETCH_SIZE+WRITE_SIZE)*1024, gfx950 FETCH_SIZE correction"},
                               f, indent=1)
     with open(os.path.join(outdir, f"{tag}_profile_summary.json"), "w") as f:
