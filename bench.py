@@ -31,7 +31,7 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-PKG_DIR = os.path.join(ROOT, "hw-accelerator-three-sequence-alignment_amd")
+PKG_DIR = os.environ.get("TSA_PKG_DIR", os.path.join(ROOT, "hw-accelerator-three-sequence-alignment_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 BYTES_PER_CELL = 28            # 7 int16 states written + read once
@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target wall time of the CPU-baseline sample")
     ap.add_argument("--check", type=int, default=4, help="triples checked vs the oracle")
+    ap.add_argument("--score-bits", type=int, default=12,
+                    help="12 = RTL wrap (default); 16/0 for cubes beyond the RTL envelope (1024^3)")
     args = ap.parse_args()
 
     import torch
@@ -105,7 +107,7 @@ def main():
     n_total = per_gpu * world
     i0, i1 = shard.shard_range(n_total, rank, world)
     n = i1 - i0
-    params = tsa.TsaParams.default()
+    params = tsa.TsaParams.default(score_bits=args.score_bits)
 
     # ---- inputs resident in HBM before timing --------------------------------
     seqs, offs = synth.batch(i0, n, L)
@@ -219,7 +221,8 @@ def main():
         idx = sorted(set([0, n_total - 1] + [int(v) for v in np.linspace(0, n_total - 1, args.check)]))
         trip = [synth.triple(i, L) for i in idx]
         cs, co = tsa.pack_batch(trip)
-        ref = oracle.score_batch(cs, co, oracle.default_params(), nthreads=nthreads)
+        oparams = oracle.default_params(score_bits=args.score_bits)
+        ref = oracle.score_batch(cs, co, oparams, nthreads=nthreads)
         got = all_scores[idx]
         parity = {"checked": len(idx), "mismatches": int((ref != got).sum()),
                   "against": "oracle/tsa_oracle.c"}
@@ -228,13 +231,13 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             # bounded sample of the same workload: one 256^3 triple per thread per round
             t_one = oracle.now()
-            oracle.score_batch(cs[: 3 * L], co[:4], oracle.default_params(), nthreads=1)
+            oracle.score_batch(cs[: 3 * L], co[:4], oparams, nthreads=1)
             t_one = oracle.now() - t_one
             rounds = max(1, int(args.cpu_seconds / max(t_one, 1e-3)))
             ns = nthreads * rounds
             bs, bo = synth.batch(0, ns, L)
             t = oracle.now()
-            oracle.score_batch(bs, bo, oracle.default_params(), nthreads=nthreads)
+            oracle.score_batch(bs, bo, oparams, nthreads=nthreads)
             t = oracle.now() - t
             cpu_baseline = {
                 "value": round(ns * cells_per_triple / t / 1e9, 5), "unit": "GCUPS",

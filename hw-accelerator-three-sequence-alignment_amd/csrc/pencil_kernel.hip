@@ -46,11 +46,13 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 // waves (= DP rows) per lap: 16 (one 1024-thread WG per CU) or 8 (two WGs
 // per CU, so one computes while the other waits at its per-step barrier)
 constexpr int PENCIL_NW_DEFAULT = 8;
-constexpr int PD = 8;              // LDS-DMA prefetch distance of wave 0, steps
-constexpr int LPD = 4;             // prefetch distance of the lap kernel (cross-CU hand-off)
 constexpr int STORE_SLACK = 4;     // last wave keeps <= this many steps of stores in flight
-constexpr int PMIN = 48;           // >= PD + NW + STORE_SLACK + margin
-constexpr int MAX_LA = 4096, MAX_LB = 4096;
+constexpr int MAX_LA = 4096, MAX_LB = 4096, MAX_LC = 1024;
+constexpr size_t LDS_MAX = 160 * 1024;
+// LDS-DMA prefetch distance (steps) of wave 0: helix (ring) and lap (hand-off);
+// shorter for wide positions (M pairs per lane) so the record slots fit in LDS
+__host__ __device__ constexpr int helix_pd(int M) { return M >= 8 ? 2 : M >= 4 ? 4 : 8; }
+__host__ __device__ constexpr int lap_pd(int M) { return M >= 8 ? 3 : 4; }
 constexpr int REC_BYTES = 16;      // {Iy, Ixy, Iyz, best} packed pairs per lane
 constexpr int RING_EXTRA = 8;
 
@@ -74,23 +76,40 @@ struct PencilGeom {
   int64_t ring_bytes_per_triple;
 };
 
-static inline int32_t pencil_pairs(int32_t max_lc) { return max_lc <= 128 ? 1 : 2; }
+// positions per lane: M packed pairs cover LC <= 128*M (1, 2, 4 or 8)
+static inline int32_t pencil_pairs(int32_t max_lc) {
+  return max_lc <= 128 ? 1 : max_lc <= 256 ? 2 : max_lc <= 512 ? 4 : 8;
+}
+// waves per CU the VGPR budget allows: 4 per SIMD up to M = 2, 2 beyond
+static int waves_per_cu(int M) { return M >= 4 ? 8 : 16; }
 
+// Helix rows per workgroup: 8 (two WGs per CU) or 16; M >= 4 always 8.
+static int helix_nw(int M) {
+  if (M >= 4) return 8;
+  if (const char *e = getenv("TSA_PENCIL_NW")) return atoi(e) == 16 ? 16 : 8;  // tuning knob
+  return PENCIL_NW_DEFAULT;
+}
 static PencilGeom pencil_geom(int32_t max_la, int32_t max_lc) {
   PencilGeom g;
   g.M = pencil_pairs(max_lc);
-  const int32_t zt = 128 * g.M;
-  g.P = std::max(std::max(max_la, zt), PMIN);
+  g.P = std::max(max_la, 128 * g.M);  // >= 128 > NW + helix_pd + STORE_SLACK: ring lag
   g.R = g.P + RING_EXTRA;
   g.ring_bytes_per_triple = (int64_t)g.R * g.M * 64 * REC_BYTES;
   return g;
+}
+static size_t helix_lds(int M, int NW, int32_t P, int32_t max_lb) {
+  return (size_t)(NW - 1) * 2 * M * 1024 + (size_t)helix_pd(M) * M * 1024 +
+         4 * ((size_t)P + 128 * M) + 4 * (((size_t)max_lb + 3) & ~(size_t)3) + (size_t)M * 256;
 }
 
 bool pencil_supported(const tsa_params *p) { return p != nullptr; }
 
 static bool pencil_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc) {
-  return max_la >= 1 && max_la <= MAX_LA && max_lb >= 1 && max_lb <= MAX_LB && max_lc >= 1 &&
-         max_lc <= 256;
+  if (!(max_la >= 1 && max_la <= MAX_LA && max_lb >= 1 && max_lb <= MAX_LB && max_lc >= 1 &&
+        max_lc <= MAX_LC))
+    return false;
+  const PencilGeom g = pencil_geom(max_la, max_lc);
+  return helix_lds(g.M, helix_nw(g.M), g.P, max_lb) <= LDS_MAX;  // the helix is always runnable
 }
 
 // Lap-parallel mode (pencil_lap_kernel) for small batches of tall cubes: every
@@ -98,43 +117,46 @@ static bool pencil_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc) {
 // Rows per lap (waves per workgroup) of the lap kernel: fewer rows = shorter
 // steps but more laps, each adding a hand-off lag. Tuning knob TSA_LAP_NW.
 constexpr int LAP_NW_DEFAULT = 16;
-static int lap_nw() {
-  if (const char *e = getenv("TSA_LAP_NW")) {
-    const int v = atoi(e);
-    if (v == 4 || v == 8 || v == 16) return v;
-  }
+static int lap_nw(int M) {
+  if (M >= 4) return 8;
+  if (const char *e = getenv("TSA_LAP_NW")) return atoi(e) == 8 ? 8 : 16;
   return LAP_NW_DEFAULT;
 }
-// workgroups guaranteed co-resident: one per CU for 16 waves, two for 8, four for 4
-static int max_resident_wg(int nw) { return 256 * (16 / nw); }
+static size_t lap_lds(int M, int NW, int32_t max_la, int32_t max_lc) {
+  return (size_t)(NW - 1) * 2 * M * 1024 + (size_t)lap_pd(M) * (M * 1024 + 4) + (size_t)M * 256 +
+         4 * (((size_t)max_la + max_lc + NW + 128 * M + 3) & ~(size_t)3);
+}
 struct LapGeom {
-  int32_t NW, G, YR;
-  size_t yf_bytes, flag_bytes;
+  int32_t M, NW, G, YR;
+  size_t lds, yf_bytes, flag_bytes;
 };
 static LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
   LapGeom g;
-  const int32_t M = pencil_pairs(max_lc);
-  g.NW = lap_nw();
+  g.M = pencil_pairs(max_lc);
+  g.NW = lap_nw(g.M);
   g.G = (max_lb + g.NW - 1) / g.NW;
-  g.YR = max_la + max_lc + 2 * g.NW + PD + 8;
-  g.yf_bytes = (size_t)n * g.G * g.YR * M * 64 * REC_BYTES;
+  g.YR = max_la + max_lc + 2 * g.NW + 16;
+  g.lds = lap_lds(g.M, g.NW, max_la, max_lc);
+  g.yf_bytes = (size_t)n * g.G * g.YR * g.M * 64 * REC_BYTES;
   g.flag_bytes = (((size_t)n * g.G + 1) * sizeof(int32_t) + 255) & ~(size_t)255;
   return g;
 }
-static bool use_lap_mode(int32_t n, int32_t max_lb) {
+// every workgroup of a lap-mode grid must be co-resident (spinning consumers)
+static bool use_lap_mode(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
   if (const char *e = getenv("TSA_PENCIL_MODE")) {
     if (!strcmp(e, "helix")) return false;
   }
-  const int nw = lap_nw();
-  const int32_t G = (max_lb + nw - 1) / nw;
-  return G >= 2 && (int64_t)n * G <= max_resident_wg(nw);
+  const LapGeom g = lap_geom(1, max_la, max_lb, max_lc);
+  if (g.lds > LDS_MAX || g.G < 2) return false;
+  const int64_t per_cu = std::min<int64_t>(LDS_MAX / g.lds, waves_per_cu(g.M) / g.NW);
+  return (int64_t)n * g.G <= 256 * per_cu;
 }
 
 size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
   if (!pencil_shape_ok(max_la, max_lb, max_lc)) return 0;
   const size_t helix = (size_t)std::min<int32_t>(n, 65535) *
                        (size_t)pencil_geom(max_la, max_lc).ring_bytes_per_triple;
-  if (use_lap_mode(n, max_lb)) {  // the lap kernel unless the params need int16
+  if (use_lap_mode(n, max_la, max_lb, max_lc)) {
     const LapGeom g = lap_geom(n, max_la, max_lb, max_lc);
     return std::max(helix, g.flag_bytes + g.yf_bytes);
   }
@@ -375,11 +397,23 @@ __device__ __forceinline__ void zshift(uint32_t (&v)[M], const uint32_t (&src)[M
   v[0] = bfi(mask0, face, v[0]);
 }
 
+// The step lambdas are left to the regular inliner for M <= 2 (an early forced
+// inline costs ~7 % there); for M >= 4 the inliner gives up on their size and
+// the captured state would spill to scratch, so those calls are forced inline.
+#define TSA_INLINE_IF_WIDE(call)                 \
+  do {                                           \
+    if constexpr (M >= 4) {                      \
+      [[clang::always_inline]] call;             \
+    } else {                                     \
+      call;                                      \
+    }                                            \
+  } while (0)
+
 // ---------------------------------------------------------------------------
 // Helix kernel: one workgroup per triple (grid-stride over the batch).
 //   LDS: xr  [NW-1][2][M][64][16]  wave w -> w+1 records {Iy, Ixy, Iyz, best}
-//        xr0 [PD][M][64][16]       ring rows prefetched for wave 0 (LDS-DMA)
-//        sA2 [P+256] u32           A codes for positions k and k+64 of one pair
+//        xr0 [PD][M][64][16]       ring rows prefetched for wave 0 (LDS-DMA), PD = helix_pd(M)
+//        sA2 [P+ZT] u32            A codes for positions k and k+64 of one pair
 //        sB  [LB] u32              B code, both halves
 //        fin [M][64] u32           best of the final step (wave w_f)
 // F16 selects the exact-f16 arithmetic above, else the int16 form.
@@ -396,6 +430,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
   constexpr int PAIR_BYTES = 64 * REC_BYTES;  // one pair's record, 1 KiB
   constexpr int SLOT_BYTES = M * PAIR_BYTES;
   constexpr int ZT = 128 * M;
+  constexpr int PD = helix_pd(M);
   uint8_t *xr = smem;
   uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT_BYTES;
   uint32_t *sA2 = (uint32_t *)(xr0 + PD * SLOT_BYTES);
@@ -412,9 +447,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
   uint32_t fsv = pa.f_single, fpv = pa.f_pair;  // VGPR copies for v_bfi_b32 / v_pk_mad_u16
   uint32_t sbcv = pa.h_sbc, kdv = pa.h_kd, k0v = pa.h_k0, one1 = 0x00010001u;
   asm volatile("" : "+v"(fsv), "+v"(fpv), "+v"(sbcv), "+v"(kdv), "+v"(k0v), "+v"(one1));
-  // a[i] of this lane at step t is sA2[(t-w) mod P + 256 - lane - 128 i]
+  // a[i] of this lane at step t is sA2[(t-w) mod P + ZT - lane - 128 i]
   const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
-                          4u * (uint32_t)(256 - lane - 128 * (M - 1));
+                          4u * (uint32_t)(ZT - lane - 128 * (M - 1));
 
   for (int tri = blockIdx.x; tri < n; tri += gridDim.x) {
     const int64_t o0 = offs[3 * (int64_t)tri], o1 = offs[3 * (int64_t)tri + 1];
@@ -423,8 +458,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     uint8_t *ring = ring_base + (int64_t)blockIdx.x * ring_stride;
 
     // ---- stage A codes (padded to P, pairs k/k+64) and B; face records in the ring
-    for (int j = threadIdx.x; j < P + 256; j += 64 * NW) {
-      const int x0 = ((j - 256) % P + P) % P, x1 = ((j - 320) % P + P) % P;
+    for (int j = threadIdx.x; j < P + ZT; j += 64 * NW) {
+      const int x0 = ((j - ZT) % P + P) % P, x1 = ((j - ZT - 64) % P + P) % P;
       const uint32_t c0 = x0 < la ? SYM0 << (seqs[o0 + x0] & 3) : 0u;
       const uint32_t c1 = x1 < la ? SYM0 << (seqs[o0 + x1] & 3) : 0u;
       sA2[j] = c0 | (c1 << 16);
@@ -549,6 +584,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       // VALU issue goes by priority then age, so without this the oldest waves
       // of a SIMD finish each step first and idle at the barrier (+3-4 %).
       __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);  // keep the arithmetic between the two
+      __builtin_amdgcn_sched_barrier(0);  // keep the arithmetic between the two
       if constexpr (F16)
         cell_messages_f16<M, SOP>(a, b, c, SBC, K, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx,
                              oIy, oIz, oIxy, oIyz, oIxz, oBest);
@@ -556,7 +593,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         cell_messages<M, SOP ? 1 : 0>(a, b, c, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz,
                                       inM, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
 
-      __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
       // ---- the final cell (src/TriAlign_1cyc.v:141-142,342-345) is in wave w_f's
       // last step; it is read back after the loop
       if (t == T - 1 && w == w_f) {
@@ -628,14 +667,14 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       int32_t t = 0;
 #pragma unroll 1
       for (; t + 1 < T; t += 2) {
-        step(std::integral_constant<int, 0>{}, role, t);
-        step(std::integral_constant<int, 1>{}, role, t + 1);
+        TSA_INLINE_IF_WIDE(step(std::integral_constant<int, 0>{}, role, t));
+        TSA_INLINE_IF_WIDE(step(std::integral_constant<int, 1>{}, role, t + 1));
       }
-      if (t < T) step(std::integral_constant<int, 0>{}, role, t);
+      if (t < T) TSA_INLINE_IF_WIDE(step(std::integral_constant<int, 0>{}, role, t));
     };
-    if (w == 0) run(std::integral_constant<int, 0>{});
-    else if (w == NW - 1) run(std::integral_constant<int, 2>{});
-    else run(std::integral_constant<int, 1>{});
+    if (w == 0) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 0>{}));
+    else if (w == NW - 1) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 2>{}));
+    else TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 1>{}));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -669,7 +708,7 @@ __device__ __forceinline__ void store16_sc1(void *gptr, uint4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(gptr), "v"(d) : "memory");
 }
 
-template <int M, int NW, bool SOP>
+template <int M, int NW, bool F16, bool SOP>
 __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     const uint8_t *__restrict__ seqs, const int64_t *__restrict__ offs, int32_t G, int32_t YR,
     int32_t lds_a, uint8_t *__restrict__ yf_base, int32_t *__restrict__ flags,
@@ -678,18 +717,20 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
   constexpr int PAIR_BYTES = 64 * REC_BYTES;
   constexpr int SLOT_BYTES = M * PAIR_BYTES;
   constexpr int ZT = 128 * M;
+  constexpr int LPD = lap_pd(M);
   uint8_t *xr = smem;                                    // [NW-1][2][M][64][16]
   uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT_BYTES;         // [LPD][M][64][16]
   int32_t *fslot = (int32_t *)(xr0 + LPD * SLOT_BYTES);  // [LPD] prefetched producer flags
   uint32_t *fin = (uint32_t *)(fslot + LPD);             // [M][64] final-step best
-  uint32_t *sA2 = fin + M * 64;                          // [la + lc + NW + 256] A code pairs
+  uint32_t *sA2 = fin + M * 64;                          // [la + lc + NW + ZT] A code pairs
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t sel = lane == 0 ? 0x05040302u : 0x07060504u;
   const uint32_t mask0 = lane == 0 ? 0x0000FFFFu : 0u;
-  uint32_t Q = 0x08000800u, fsv = pa.f_single, fpv = pa.f_pair;
+  uint32_t Q = F16 ? 0x08000800u : 0x00010001u, fsv = pa.f_single, fpv = pa.f_pair;
   asm volatile("" : "+v"(Q), "+v"(fsv), "+v"(fpv));
+  const PencilArgs pv = F16 ? pa : pin_score_consts(pa);
 
   const int32_t tri = blockIdx.x / G, L = blockIdx.x % G;
   const int64_t o0 = offs[3 * (int64_t)tri], o1 = offs[3 * (int64_t)tri + 1];
@@ -706,18 +747,18 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
   int32_t *flag_mine = flags + (int64_t)tri * G + L;
   const int32_t *flag_prev = flag_mine - 1;
 
-  // A code pairs: entry j holds x = j-256 (lo) and x = j-320 (hi), 0 outside [0, la)
+  // A code pairs: entry j holds x = j-ZT (lo) and x = j-ZT-64 (hi), 0 outside [0, la)
   const int32_t na = lds_a / 4;
   for (int j = threadIdx.x; j < na; j += 64 * NW) {
-    const int x0 = j - 256, x1 = j - 320;
+    const int x0 = j - ZT, x1 = j - ZT - 64;
     const uint32_t c0 = (x0 >= 0 && x0 < la) ? SYM0 << (seqs[o0 + x0] & 3) : 0u;
     const uint32_t c1 = (x1 >= 0 && x1 < la) ? SYM0 << (seqs[o0 + x1] & 3) : 0u;
     sA2[j] = c0 | (c1 << 16);
   }
   __syncthreads();
-  // position k of this wave is at x-1 = t - w - k: a[i] = sA2[t - w + 256 - lane - 128 i]
+  // position k of this wave is at x-1 = t - w - k: a[i] = sA2[t - w + ZT - lane - 128 i]
   const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
-                          4u * (uint32_t)(256 - w - lane - 128 * (M - 1));
+                          4u * (uint32_t)(ZT - w - lane - 128 * (M - 1));
 
   const int32_t y = L * NW + w + 1;  // this wave's DP row
   const uint32_t bw = y <= lb ? (SYM0 << (seqs[o1 + y - 1] & 3)) * 0x00010001u : 0u;
@@ -744,7 +785,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
 
   // wave 0 of lap L>0: row r of yf_prev feeds step r - (NW-1); prime LPD steps
   int32_t seen = 0;  // rows of yf_prev known complete
-  auto ensure = [&](int32_t r) {  // row r must be published (r < the producer's T)
+  auto ensure = [&](int32_t r) __attribute__((always_inline)) {  // row r must be published (r < the producer's T)
     if (r < seen) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (uint32_t spin = 0;; ++spin) {
@@ -760,7 +801,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     }
   };
   const int32_t T_prev = la + (NW - 1) + (lc - 1);  // rows lap L-1 publishes
-  auto fetch = [&](int32_t s2) {  // rows of step s2 -> xr0 slot s2 % LPD
+  auto fetch = [&](int32_t s2) __attribute__((always_inline)) {  // rows of step s2 -> xr0 slot s2 % LPD
     const int32_t r = s2 + NW - 1;
     if (r < T_prev) ensure(r);
     const int32_t rr = r < T_prev ? r : T_prev - 1;  // past the end: any valid row
@@ -833,8 +874,14 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     }
     uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
     __builtin_amdgcn_s_setprio(0);
-    cell_messages_f16<M, SOP>(a, b, c, SBC, K, Q, pa, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM,
-                              nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
+    __builtin_amdgcn_sched_barrier(0);  // keep the arithmetic between the two
+    if constexpr (F16)
+      cell_messages_f16<M, SOP>(a, b, c, SBC, K, Q, pa, inIx, inIy, inIz, inIxy, inIyz, inIxz,
+                                inM, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
+    else
+      cell_messages<M, SOP ? 1 : 0>(a, b, c, Q, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM,
+                                    nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
+    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
     if (final_lap && t == T - 1 && w == w_f) {
 #pragma unroll
@@ -878,18 +925,18 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     int32_t t = 0;
 #pragma unroll 1
     for (; t + 1 < T; t += 2) {
-      step(std::integral_constant<int, 0>{}, role, t);
-      step(std::integral_constant<int, 1>{}, role, t + 1);
+      TSA_INLINE_IF_WIDE(step(std::integral_constant<int, 0>{}, role, t));
+      TSA_INLINE_IF_WIDE(step(std::integral_constant<int, 1>{}, role, t + 1));
     }
-    if (t < T) step(std::integral_constant<int, 0>{}, role, t);
+    if (t < T) TSA_INLINE_IF_WIDE(step(std::integral_constant<int, 0>{}, role, t));
   };
   if (w == 0) {
-    if (L == 0) run(std::integral_constant<int, 0>{});
-    else run(std::integral_constant<int, 1>{});
+    if (L == 0) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 0>{}));
+    else TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 1>{}));
   } else if (w == NW - 1) {
-    run(std::integral_constant<int, 3>{});
+    TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 3>{}));
   } else {
-    run(std::integral_constant<int, 2>{});
+    TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 2>{}));
   }
   if (w == NW - 1) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -901,8 +948,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     if (threadIdx.x == 0) {
       const int32_t l_f = k_f & 63, i_f = k_f >> 7, h_f = (k_f >> 6) & 1;
       const uint32_t v = fin[i_f * 64 + l_f];
-      scores[tri] = (int32_t)(float)__builtin_bit_cast(
-          _Float16, (uint16_t)(h_f ? (v >> 16) : (v & 0xFFFF)));
+      const uint16_t hb = (uint16_t)(h_f ? (v >> 16) : (v & 0xFFFF));
+      scores[tri] = F16 ? (int32_t)(float)__builtin_bit_cast(_Float16, hb) : (int32_t)(int16_t)hb;
     }
   }
 }
@@ -978,11 +1025,10 @@ template <int M, int NW, bool F16, bool SOP>
 static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                     int32_t max_lb, const PencilGeom &g, int32_t *d_scores, void *d_ws,
                     const PencilArgs &pa, hipStream_t stream) {
-  const int32_t lds_a = 4 * (g.P + 256), lds_b = 4 * ((max_lb + 3) & ~3);
-  const size_t lds = (size_t)(NW - 1) * 2 * M * 1024 + (size_t)PD * M * 1024 + lds_a + lds_b +
-                     (size_t)M * 64 * 4;
+  const int32_t lds_a = 4 * (g.P + 128 * M), lds_b = 4 * ((max_lb + 3) & ~3);
+  const size_t lds = helix_lds(M, NW, g.P, max_lb);
   auto kfn = pencil_kernel<M, NW, F16, SOP>;
-  if (lds > 160 * 1024) return TSA_EINVAL;
+  if (lds > LDS_MAX) return TSA_EINVAL;
   if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return TSA_EDEVICE;
@@ -993,15 +1039,14 @@ static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
   return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
 }
 
-template <int M, int NW, bool SOP>
+template <int M, int NW, bool F16, bool SOP>
 static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, int32_t max_la,
                       int32_t max_lc, const LapGeom &g, int32_t *d_scores, void *d_ws,
                       const PencilArgs &pa, hipStream_t stream) {
-  const int32_t lds_a = 4 * ((max_la + max_lc + NW + 256 + 3) & ~3);
-  const size_t lds = (size_t)(NW - 1) * 2 * M * 1024 + (size_t)LPD * M * 1024 + LPD * 4 +
-                     (size_t)M * 64 * 4 + lds_a;
-  auto kfn = pencil_lap_kernel<M, NW, SOP>;
-  if (lds > 160 * 1024) return TSA_EINVAL;
+  const int32_t lds_a = 4 * ((max_la + max_lc + NW + 128 * M + 3) & ~3);
+  const size_t lds = lap_lds(M, NW, max_la, max_lc);
+  auto kfn = pencil_lap_kernel<M, NW, F16, SOP>;
+  if (lds > LDS_MAX) return TSA_EINVAL;
   if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return TSA_EDEVICE;
@@ -1013,6 +1058,21 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
   return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
 }
 
+// Instantiated shapes: M = 1, 2 with 8 or 16 rows per workgroup; M = 4, 8
+// (LC up to 512 / 1024) with 8; each in f16 / int16 arithmetic and RTL / SOP s3.
+#define TSA_SHAPES(LAUNCH, M_, NW_, F16_, SOP_, ...)                                      \
+  ((M_) == 1 ? ((NW_) == 16 ? TSA_ARITH(LAUNCH, 1, 16, F16_, SOP_, __VA_ARGS__)            \
+                            : TSA_ARITH(LAUNCH, 1, 8, F16_, SOP_, __VA_ARGS__))            \
+   : (M_) == 2 ? ((NW_) == 16 ? TSA_ARITH(LAUNCH, 2, 16, F16_, SOP_, __VA_ARGS__)          \
+                              : TSA_ARITH(LAUNCH, 2, 8, F16_, SOP_, __VA_ARGS__))          \
+   : (M_) == 4 ? TSA_ARITH(LAUNCH, 4, 8, F16_, SOP_, __VA_ARGS__)                          \
+               : TSA_ARITH(LAUNCH, 8, 8, F16_, SOP_, __VA_ARGS__))
+#define TSA_ARITH(LAUNCH, MM, NN, F16_, SOP_, ...)                                        \
+  ((F16_) ? ((SOP_) ? LAUNCH<MM, NN, true, true>(__VA_ARGS__)                              \
+                    : LAUNCH<MM, NN, true, false>(__VA_ARGS__))                            \
+          : ((SOP_) ? LAUNCH<MM, NN, false, true>(__VA_ARGS__)                             \
+                    : LAUNCH<MM, NN, false, false>(__VA_ARGS__)))
+
 int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                         int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
                         const Range &bound, int32_t *d_scores, void *d_ws, size_t ws_bytes,
@@ -1021,37 +1081,20 @@ int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t
   if (!pencil_shape_ok(max_la, max_lb, max_lc)) return TSA_EINVAL;
   const bool f16 = use_f16(kp, bound);
   const PencilArgs pa = make_args(kp, f16);
-  if (f16 && use_lap_mode(n, max_lb)) {  // the lap kernel is f16-only; else helix
+  const bool sop = pa.sop != 0;
+  if (use_lap_mode(n, max_la, max_lb, max_lc)) {
     const LapGeom lg = lap_geom(n, max_la, max_lb, max_lc);
     if (ws_bytes < lg.flag_bytes + lg.yf_bytes) return TSA_ENOMEM;
-#define TSA_LAP(MM, NN)                                                                    \
-  (pa.sop ? launch_lap<MM, NN, true>(d_seqs, d_offsets, n, max_la, max_lc, lg, d_scores, d_ws, \
-                                     pa, stream)                                           \
-          : launch_lap<MM, NN, false>(d_seqs, d_offsets, n, max_la, max_lc, lg, d_scores,   \
-                                      d_ws, pa, stream))
-    if (pencil_pairs(max_lc) == 1)
-      return lg.NW == 4 ? TSA_LAP(1, 4) : lg.NW == 8 ? TSA_LAP(1, 8) : TSA_LAP(1, 16);
-    return lg.NW == 4 ? TSA_LAP(2, 4) : lg.NW == 8 ? TSA_LAP(2, 8) : TSA_LAP(2, 16);
-#undef TSA_LAP
+    return TSA_SHAPES(launch_lap, lg.M, lg.NW, f16, sop, d_seqs, d_offsets, n, max_la, max_lc,
+                      lg, d_scores, d_ws, pa, stream);
   }
   const PencilGeom g = pencil_geom(max_la, max_lc);
   const int32_t grid = n < 65535 ? n : 65535;
   if (ws_bytes < (size_t)grid * (size_t)g.ring_bytes_per_triple) return TSA_ENOMEM;
-  int nw = PENCIL_NW_DEFAULT;
-  if (const char *e = getenv("TSA_PENCIL_NW")) {  // tuning knob
-    const int v = atoi(e);
-    nw = (v == 4 || v == 8) ? v : 16;
-  }
-#define TSA_HELIX(MM, NN, FF, SS) \
-  launch_m<MM, NN, FF, SS>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_ws, pa, stream)
-#define TSA_HELIX_F(MM, NN)                                                           \
-  (f16 ? (pa.sop ? TSA_HELIX(MM, NN, true, true) : TSA_HELIX(MM, NN, true, false))   \
-       : (pa.sop ? TSA_HELIX(MM, NN, false, true) : TSA_HELIX(MM, NN, false, false)))
-  if (g.M == 1)
-    return nw == 4 ? TSA_HELIX_F(1, 4) : nw == 8 ? TSA_HELIX_F(1, 8) : TSA_HELIX_F(1, 16);
-  return nw == 4 ? TSA_HELIX_F(2, 4) : nw == 8 ? TSA_HELIX_F(2, 8) : TSA_HELIX_F(2, 16);
-#undef TSA_HELIX_F
-#undef TSA_HELIX
+  return TSA_SHAPES(launch_m, g.M, helix_nw(g.M), f16, sop, d_seqs, d_offsets, n, max_lb, g,
+                    d_scores, d_ws, pa, stream);
 }
+#undef TSA_SHAPES
+#undef TSA_ARITH
 
 }  // namespace tsa

@@ -140,6 +140,26 @@ def test_pencil_shapes_vs_oracle(gpu, orc):
         assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (la, lb, lc)
 
 
+@pytest.mark.parametrize("mode", ["helix", "lap"])
+def test_pencil_wide_positions(gpu, orc, monkeypatch, mode):
+    # LC > 256: M = 4 or 8 packed pairs per lane (2 waves per SIMD), both the
+    # batch helix and the single-cube lap kernel, f16 and int16 arithmetic
+    if mode == "helix":
+        monkeypatch.setenv("TSA_PENCIL_MODE", "helix")
+    rng = np.random.default_rng(90 if mode == "helix" else 91)
+    # 16-bit words: beyond ~680 per side the 12-bit RTL bound no longer holds
+    p, op = gpu.TsaParams.default(score_bits=16), orc.default_params(score_bits=16)
+    for la, lb, lc in [(64, 20, 257), (300, 33, 512), (40, 17, 513), (257, 40, 700),
+                       (130, 24, 1024), (600, 9, 1000)]:
+        a, b, c = (rng.integers(0, 4, n).astype(np.uint8) for n in (la, lb, lc))
+        assert gpu.score(a, b, c, p, kernel="pencil") == orc.score(a, b, c, op), (mode, la, lb, lc)
+    a = rng.integers(0, 4, 700).astype(np.uint8)
+    b = a[:64].copy()
+    c = a.copy()
+    c[::9] = (c[::9] + 1) % 4  # related: scores beyond 2048 need the int16 form
+    assert gpu.score(a, b, c, p, kernel="pencil") == orc.score(a, b, c, op), mode
+
+
 @pytest.mark.parametrize("nw", ["8", "16"])
 def test_pencil_waves_per_workgroup(gpu, orc, monkeypatch, nw):
     monkeypatch.setenv("TSA_PENCIL_NW", nw)
@@ -197,7 +217,7 @@ def test_pencil_single_cube_modes(gpu, orc, synth, monkeypatch, mode):
         assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (mode, la, lb, lc)
 
 
-@pytest.mark.parametrize("nw", ["4", "8"])
+@pytest.mark.parametrize("nw", ["8", "16"])
 def test_pencil_lap_rows_per_lap(gpu, orc, synth, monkeypatch, nw):
     monkeypatch.setenv("TSA_LAP_NW", nw)
     rng = np.random.default_rng(40 + int(nw))
@@ -265,3 +285,13 @@ def test_batch_async_device_pointers(gpu, orc, synth):
                               kernel=kernel)
         torch.cuda.synchronize()
         assert np.array_equal(d_scores.cpu().numpy(), orc.score_batch(seqs, offs, nthreads=6))
+
+
+def test_1024_cube_config_c4(gpu, orc, synth):
+    # configs[3]: one 1024^3 synthetic triple, 16-bit words (beyond the RTL's
+    # 512 envelope the 12-bit wrap is not meaningful); lap kernel with 8 packed
+    # pairs per lane. The oracle needs ~30 s of one CPU core.
+    a, b, c = synth.triple(0, 1024)
+    p, op = gpu.TsaParams.default(score_bits=16), orc.default_params(score_bits=16)
+    assert gpu.score(a, b, c, p, kernel="pencil") == orc.score(a, b, c, op)
+

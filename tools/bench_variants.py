@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--kernel", default="pencil")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--score-bits", type=int, default=12)
     args = ap.parse_args()
     import torch
     import bench
@@ -32,7 +33,7 @@ def main():
     seqs, offs = synth.batch(0, n, L)
     d_seqs, d_offs = torch.from_numpy(seqs).cuda(), torch.from_numpy(offs).cuda()
     d_scores = torch.zeros(n, dtype=torch.int32, device="cuda")
-    p = tsa.TsaParams.default()
+    p = tsa.TsaParams.default(score_bits=args.score_bits)
     ws = 0
     keys = sorted({kv.split("=", 1)[0] for v in args.variants for kv in v.split(",") if kv})
 
@@ -76,7 +77,7 @@ def main():
         idx = list(range(0, n, max(1, n // 8)))
         trip = [synth.triple(i, L) for i in idx]
         cs, co = tsa.pack_batch(trip)
-        ref = oracle.score_batch(cs, co, nthreads=8)
+        ref = oracle.score_batch(cs, co, oracle.default_params(score_bits=args.score_bits), nthreads=8)
     for v in args.variants:
         med = statistics.median(times[v])
         rec = {"variant": v, "n": n, "L": L, "median_ms": round(med, 4), "min_ms": round(min(times[v]), 4),
