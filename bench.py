@@ -77,6 +77,8 @@ def main():
     ap.add_argument("--per-gpu", type=int, default=512)
     ap.add_argument("--length", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="skip the configs[1]/configs[3] single-cube timings")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target wall time of the CPU-baseline sample")
     ap.add_argument("--check", type=int, default=4, help="triples checked vs the oracle")
@@ -181,23 +183,22 @@ def main():
                 "lane_insts_per_cell": round(insts * 64 / per_gpu_cells, 3),
                 "source": f"SQ_INSTS_VALU, profiles/pmc_{kernel_name}_{args.workload}.json"}
 
-    # single-cube latency, configs[2]
-    single = None
-    try:
-        sa = synth.batch(0, 1, L)
+    # single-cube latency: configs[2] (L^3, params as the batch), plus configs[1]
+    # (64^3) and configs[3] (1024^3, 16-bit words: beyond the RTL envelope)
+    def time_single(Ls, prm, reps=5):
+        sa = synth.batch(0, 1, Ls)
         s_seqs = torch.from_numpy(sa[0]).to(dev)
         s_offs = torch.from_numpy(sa[1]).to(dev)
         s_score = torch.zeros(1, dtype=torch.int32, device=dev)
-        s_ws = tsa.workspace_size(1, L, L, L, params, args.kernel)
+        s_ws = tsa.workspace_size(1, Ls, Ls, Ls, prm, args.kernel)
         s_wsb = torch.empty(max(s_ws, 16), dtype=torch.uint8, device=dev)
 
         def sstep():
-            tsa.score_batch_async(s_seqs.data_ptr(), s_offs.data_ptr(), 1, L, L, L,
+            tsa.score_batch_async(s_seqs.data_ptr(), s_offs.data_ptr(), 1, Ls, Ls, Ls,
                                   s_score.data_ptr(), s_wsb.data_ptr(), s_ws, stream.cuda_stream,
-                                  params, args.kernel)
+                                  prm, args.kernel)
         sstep()
         torch.cuda.synchronize()
-        reps = 5
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(reps):
@@ -205,9 +206,17 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize()
         sms = e0.elapsed_time(e1) / reps
-        single = {"config": f"configs[2]: one {L}^3 triple", "ms": round(sms, 4),
-                  "gcups": round(cells_per_triple / (sms * 1e-3) / 1e9, 3),
-                  "score": int(s_score.item())}
+        return {"ms": round(sms, 4), "gcups": round(Ls ** 3 / (sms * 1e-3) / 1e9, 3),
+                "score": int(s_score.item()), "score_bits": prm.score_bits}
+
+    single = None
+    other_configs = {}
+    try:
+        single = {"config": f"configs[2]: one {L}^3 triple", **time_single(L, params)}
+        if not args.no_extra_configs:
+            other_configs["configs[1]: one 64^3 triple"] = time_single(64, params, reps=10)
+            other_configs["configs[3]: one 1024^3 triple"] = time_single(
+                1024, tsa.TsaParams.default(score_bits=16), reps=3)
     except Exception as e:  # noqa: BLE001
         log("single-cube measurement failed:", e)
 
@@ -279,6 +288,7 @@ def main():
         },
         "cpu_baseline": cpu_baseline,
         "single_cube": single,
+        "other_configs": other_configs,
         "parity": parity,
     }
     print(json.dumps(out), flush=True)
