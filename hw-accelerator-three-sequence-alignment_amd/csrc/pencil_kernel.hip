@@ -52,7 +52,14 @@ constexpr size_t LDS_MAX = 160 * 1024;
 // LDS-DMA prefetch distance (steps) of wave 0: helix (ring) and lap (hand-off);
 // shorter for wide positions (M pairs per lane) so the record slots fit in LDS
 __host__ __device__ constexpr int helix_pd(int M) { return M >= 8 ? 2 : M >= 4 ? 4 : 8; }
-__host__ __device__ constexpr int lap_pd(int M) { return M >= 8 ? 3 : 4; }
+#ifndef TSA_LAP_PD  // build-time tuning knobs of the lap hand-off
+#define TSA_LAP_PD 4
+#endif
+#ifndef TSA_LAP_SLACK
+#define TSA_LAP_SLACK 4
+#endif
+__host__ __device__ constexpr int lap_pd(int M) { return M >= 8 ? (TSA_LAP_PD < 3 ? TSA_LAP_PD : 3) : TSA_LAP_PD; }
+constexpr int LAP_SLACK = TSA_LAP_SLACK;  // producer steps of row stores in flight
 constexpr int REC_BYTES = 16;      // {Iy, Ixy, Iyz, best} packed pairs per lane
 constexpr int RING_EXTRA = 8;
 
@@ -387,14 +394,17 @@ __device__ __forceinline__ void cell_messages_f16(
 // lanes >= 1 take lane-1's pair as is; lane 0 takes (pair i-1).hi and
 // (pair i).lo of lane 63; position 0 (lane 0, pair 0, lo) gets the z = 0 face.
 template <int M>
+// Only lane 0 reads the second v_perm source (its selector takes bytes 2..3 of
+// it), so for pair 0 that source is `face`, whose high half is the z = 0 face
+// (or, for a z-tile, the previous tile's last position) -- no extra v_bfi.
 __device__ __forceinline__ void zshift(uint32_t (&v)[M], const uint32_t (&src)[M], uint32_t sel,
-                                       uint32_t mask0, uint32_t face) {
+                                       uint32_t face) {
   uint32_t r[M];
 #pragma unroll
   for (int i = 0; i < M; ++i) r[i] = ror1(src[i]);
+  v[0] = __builtin_amdgcn_perm(r[0], face, sel);
 #pragma unroll
-  for (int i = 0; i < M; ++i) v[i] = __builtin_amdgcn_perm(r[i], r[(i + M - 1) % M], sel);
-  v[0] = bfi(mask0, face, v[0]);
+  for (int i = 1; i < M; ++i) v[i] = __builtin_amdgcn_perm(r[i], r[i - 1], sel);
 }
 
 // The step lambdas are left to the regular inliner for M <= 2 (an early forced
@@ -440,7 +450,6 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t sel = lane == 0 ? 0x05040302u : 0x07060504u;
-  const uint32_t mask0 = lane == 0 ? 0x0000FFFFu : 0u;
   uint32_t ones = F16 ? 0x08000800u : 0x00010001u;  // f16: match indicator 2^-13
   asm volatile("" : "+v"(ones));                     // keep it in a VGPR (VOP3P operand)
   const PencilArgs pv = F16 ? pa : pin_score_consts(pa);
@@ -638,10 +647,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       uint32_t rz[M], rw[M];
 #pragma unroll
       for (int i = 0; i < M; ++i) { rz[i] = rec[i].z; rw[i] = rec[i].w; }
-      zshift<M>(shIxz[PH], oIxz, sel, mask0, pa.f_pair);  // z = 0 face for position 0
-      zshift<M>(shIz, oIz, sel, mask0, pa.f_single);
-      zshift<M>(svIyz, rz, sel, mask0, pa.f_pair);
-      zshift<M>(svM[PH], rw, sel, mask0, 0u);
+      zshift<M>(shIxz[PH], oIxz, sel, pa.f_pair);  // z = 0 face for position 0
+      zshift<M>(shIz, oIz, sel, pa.f_single);
+      zshift<M>(svIyz, rz, sel, pa.f_pair);
+      zshift<M>(svM[PH], rw, sel, 0u);
       // position 0 advances to u0 + 1
       if (++xpos0 == P) {
         xpos0 = 0;
@@ -692,7 +701,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 // flight at once (blockIdx.x = tri * G + L). Lap L's last wave hands its
 // per-step record rows down to lap L+1's wave 0 through global memory:
 //   producer: write-through (sc1) row stores; each step a counted vmcnt proves
-//             rows <= tau-STORE_SLACK complete, then one agent-scope flag store
+//             rows <= tau-LAP_SLACK complete, then one agent-scope flag store
 //             publishes that count (MI355X_MICROARCH.md "Valid forms", row 1);
 //   consumer: the flag word travels with the rows (LDS-DMA, LPD steps ahead);
 //             only when it does not yet cover a row does wave 0 drain its
@@ -727,7 +736,6 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t sel = lane == 0 ? 0x05040302u : 0x07060504u;
-  const uint32_t mask0 = lane == 0 ? 0x0000FFFFu : 0u;
   uint32_t Q = F16 ? 0x08000800u : 0x00010001u, fsv = pa.f_single, fpv = pa.f_pair;
   asm volatile("" : "+v"(Q), "+v"(fsv), "+v"(fpv));
   const PencilArgs pv = F16 ? pa : pin_score_consts(pa);
@@ -906,17 +914,17 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     uint32_t rz[M], rw[M];
 #pragma unroll
     for (int i = 0; i < M; ++i) { rz[i] = rec[i].z; rw[i] = rec[i].w; }
-    zshift<M>(shIxz[PH], oIxz, sel, mask0, pa.f_pair);  // z = 0 face for position 0
-    zshift<M>(shIz, oIz, sel, mask0, pa.f_single);
-    zshift<M>(svIyz, rz, sel, mask0, pa.f_pair);
-    zshift<M>(svM[PH], rw, sel, mask0, 0u);
+    zshift<M>(shIxz[PH], oIxz, sel, pa.f_pair);  // z = 0 face for position 0
+    zshift<M>(shIz, oIz, sel, pa.f_single);
+    zshift<M>(svIyz, rz, sel, pa.f_pair);
+    zshift<M>(svM[PH], rw, sel, 0u);
     if constexpr (ROLE == 1) fetch(t + LPD);  // usually covered by the prefetched flag
     if constexpr (ROLE == 3) {
-      // rows <= t - STORE_SLACK complete (M stores + 1 flag store per step)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STORE_SLACK * (M + 1)) : "memory");
+      // rows <= t - LAP_SLACK complete (M stores + 1 flag store per step)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LAP_SLACK * (M + 1)) : "memory");
       // exactly M + 1 vector-memory ops per step keep that count exact
       if (lane == 0)
-        __hip_atomic_store(flag_mine, t >= STORE_SLACK ? t - STORE_SLACK + 1 : 0,
+        __hip_atomic_store(flag_mine, t >= LAP_SLACK ? t - LAP_SLACK + 1 : 0,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
