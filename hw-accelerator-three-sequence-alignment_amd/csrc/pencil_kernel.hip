@@ -35,6 +35,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "pencil_kernel.h"
 
@@ -58,7 +59,12 @@ __host__ __device__ constexpr int helix_pd(int M) { return M >= 8 ? 2 : M >= 4 ?
 #ifndef TSA_LAP_SLACK
 #define TSA_LAP_SLACK 4
 #endif
-__host__ __device__ constexpr int lap_pd(int M) { return M >= 8 ? (TSA_LAP_PD < 3 ? TSA_LAP_PD : 3) : TSA_LAP_PD; }
+#ifndef TSA_LAP_PD1  // M = 1: short steps, so more steps must cover the DMA latency
+#define TSA_LAP_PD1 TSA_LAP_PD
+#endif
+__host__ __device__ constexpr int lap_pd(int M) {
+  return M >= 8 ? (TSA_LAP_PD < 3 ? TSA_LAP_PD : 3) : M == 1 ? TSA_LAP_PD1 : TSA_LAP_PD;
+}
 constexpr int LAP_SLACK = TSA_LAP_SLACK;  // producer steps of row stores in flight
 constexpr int REC_BYTES = 16;      // {Iy, Ixy, Iyz, best} packed pairs per lane
 constexpr int RING_EXTRA = 8;
@@ -119,44 +125,67 @@ static bool pencil_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc) {
   return helix_lds(g.M, helix_nw(g.M), g.P, max_lb) <= LDS_MAX;  // the helix is always runnable
 }
 
-// Lap-parallel mode (pencil_lap_kernel) for small batches of tall cubes: every
-// lap of every triple gets its own resident workgroup.
-// Rows per lap (waves per workgroup) of the lap kernel: fewer rows = shorter
-// steps but more laps, each adding a hand-off lag. Tuning knob TSA_LAP_NW.
+// Lap-parallel mode (pencil_lap_kernel) for small batches: every (lap, z-tile)
+// of every triple gets its own resident workgroup.
+// Rows per lap (waves per workgroup): fewer rows = shorter steps but more laps,
+// each adding a hand-off lag. Tuning knob TSA_LAP_NW (8/16; M >= 4: 8).
 constexpr int LAP_NW_DEFAULT = 16;
 static int lap_nw(int M) {
   if (M >= 4) return 8;
   if (const char *e = getenv("TSA_LAP_NW")) return atoi(e) == 8 ? 8 : 16;
   return LAP_NW_DEFAULT;
 }
-static size_t lap_lds(int M, int NW, int32_t max_la, int32_t max_lc) {
-  return (size_t)(NW - 1) * 2 * M * 1024 + (size_t)lap_pd(M) * (M * 1024 + 4) + (size_t)M * 256 +
-         4 * (((size_t)max_la + max_lc + NW + 128 * M + 3) & ~(size_t)3);
+constexpr int LAP_ZRING = 16;  // = ZRING in the kernel
+static size_t lap_zrec(int NW) { return (((size_t)NW + 1) * 16 + 63) & ~(size_t)63; }
+static size_t lap_lds(int M, int NW, int32_t max_la) {
+  const int ZT = 128 * M;
+  return (size_t)(NW - 1) * 2 * M * 1024 + (size_t)lap_pd(M) * M * 1024 +
+         (4 + LAP_ZRING) * lap_zrec(NW) + 2 * (size_t)lap_pd(M) * 4 + (size_t)M * 256 +
+         4 * (((size_t)max_la + NW + 2 * ZT + 3) & ~(size_t)3);
 }
+// waves per CU for the lap kernel (M = 1 stays under 64 VGPRs: 8 waves per SIMD)
+static int lap_waves_per_cu(int M) { return M == 1 ? 32 : M == 2 ? 16 : 8; }
 struct LapGeom {
-  int32_t M, NW, G, YR;
-  size_t lds, yf_bytes, flag_bytes;
+  int32_t M, NW, G, GZ, YR;
+  size_t lds, zrec, yf_bytes, zf_bytes, flag_bytes;
+  bool ok;
 };
-static LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+static LapGeom lap_geom_m(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M) {
   LapGeom g;
-  g.M = pencil_pairs(max_lc);
-  g.NW = lap_nw(g.M);
+  g.M = M;
+  g.NW = lap_nw(M);
   g.G = (max_lb + g.NW - 1) / g.NW;
-  g.YR = max_la + max_lc + 2 * g.NW + 16;
-  g.lds = lap_lds(g.M, g.NW, max_la, max_lc);
-  g.yf_bytes = (size_t)n * g.G * g.YR * g.M * 64 * REC_BYTES;
-  g.flag_bytes = (((size_t)n * g.G + 1) * sizeof(int32_t) + 255) & ~(size_t)255;
+  g.GZ = (max_lc + 128 * M - 1) / (128 * M);
+  g.YR = max_la + 128 * M + g.NW + 16;
+  g.lds = lap_lds(M, g.NW, max_la);
+  g.zrec = lap_zrec(g.NW);
+  const size_t wgs = (size_t)n * g.G * g.GZ;
+  g.yf_bytes = wgs * g.YR * M * 64 * REC_BYTES;
+  g.zf_bytes = g.GZ > 1 ? wgs * g.YR * g.zrec : 0;
+  g.flag_bytes = ((wgs + 1) * sizeof(int32_t) + 255) & ~(size_t)255;
+  const int64_t per_cu =
+      g.lds > LDS_MAX ? 0 : std::min<int64_t>(LDS_MAX / g.lds, lap_waves_per_cu(M) / g.NW);
+  // every workgroup resident, and at least two laps or tiles to overlap
+  g.ok = (int64_t)wgs <= 256 * per_cu && (g.G >= 2 || g.GZ >= 2);
   return g;
 }
-// every workgroup of a lap-mode grid must be co-resident (spinning consumers)
+// The narrowest z-tile (128*M positions) whose grid fits; TSA_LAP_ZT forces one.
+static LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  const int m_lc = pencil_pairs(max_lc);  // one tile covers all of LC
+  if (const char *e = getenv("TSA_LAP_ZT")) {
+    const int zt = atoi(e);
+    const int M = zt <= 128 ? 1 : zt <= 256 ? 2 : zt <= 512 ? 4 : 8;
+    return lap_geom_m(n, max_la, max_lb, max_lc, std::min(M, m_lc));
+  }
+  LapGeom g = lap_geom_m(n, max_la, max_lb, max_lc, 1);
+  for (int M = 2; !g.ok && M <= m_lc; M *= 2) g = lap_geom_m(n, max_la, max_lb, max_lc, M);
+  return g;
+}
 static bool use_lap_mode(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
   if (const char *e = getenv("TSA_PENCIL_MODE")) {
     if (!strcmp(e, "helix")) return false;
   }
-  const LapGeom g = lap_geom(1, max_la, max_lb, max_lc);
-  if (g.lds > LDS_MAX || g.G < 2) return false;
-  const int64_t per_cu = std::min<int64_t>(LDS_MAX / g.lds, waves_per_cu(g.M) / g.NW);
-  return (int64_t)n * g.G <= 256 * per_cu;
+  return lap_geom(n, max_la, max_lb, max_lc).ok;
 }
 
 size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
@@ -165,7 +194,7 @@ size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t
                        (size_t)pencil_geom(max_la, max_lc).ring_bytes_per_triple;
   if (use_lap_mode(n, max_la, max_lb, max_lc)) {
     const LapGeom g = lap_geom(n, max_la, max_lb, max_lc);
-    return std::max(helix, g.flag_bytes + g.yf_bytes);
+    return std::max(helix, g.flag_bytes + g.yf_bytes + g.zf_bytes);
   }
   return helix;
 }
@@ -697,41 +726,72 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 }
 
 // ---------------------------------------------------------------------------
-// Single-cube variant: one NW-row lap per workgroup, all laps of a triple in
-// flight at once (blockIdx.x = tri * G + L). Lap L's last wave hands its
-// per-step record rows down to lap L+1's wave 0 through global memory:
-//   producer: write-through (sc1) row stores; each step a counted vmcnt proves
-//             rows <= tau-LAP_SLACK complete, then one agent-scope flag store
-//             publishes that count (MI355X_MICROARCH.md "Valid forms", row 1);
-//   consumer: the flag word travels with the rows (LDS-DMA, LPD steps ahead);
-//             only when it does not yet cover a row does wave 0 drain its
-//             queue and poll the flag with agent-scope loads.
-// Every workgroup of the grid must be resident (host: n*G <= resident WGs), so
-// a spinning consumer never blocks its producer. Spins are bounded: on
-// timeout the kernel sets *err and carries on (scores then invalid).
-// Cell arithmetic, registers and shifts are the helix kernel's (exact f16);
-// each wave owns one row, so B and the per-row score terms are constants.
+// Single-cube variant: the cube is cut into NW-row laps (y) and ZT-position
+// tiles (z, ZT = 128*M); every (lap, tile) gets its own workgroup and all of
+// them run at once (blockIdx.x = (tri * G + L) * GZ + q). Each workgroup runs
+// the helix step in its own local time t (position k of wave w at x = t-w-k+1).
+//   y hand-off: lap L's last wave stores its per-step record rows; lap L+1's
+//     wave 0 LDS-DMAs them LPD steps ahead (rows of step r feed step r-(NW-1)).
+//   z hand-off: every wave's last position (lane 63, pair M-1, hi half) leaves
+//     its {Iz, Ixz, Iyz, best} words in an LDS staging record, with wave 0
+//     adding the row above's {Iyz, best}; the last wave stores that record per
+//     step, and tile q+1's wave 0 LDS-DMAs record t+ZT for its position 0
+//     (tile q+1 runs ZT steps behind tile q, the z skew of the wavefront).
+//   producer: write-through (sc1) stores; each step a counted vmcnt proves
+//     rows <= t-LAP_SLACK (and z records two steps older) complete, then one
+//     agent-scope flag store publishes t-LAP_SLACK+1 (MI355X_MICROARCH.md
+//     "Valid forms", row 1);
+//   consumer: the flag words travel with the data (LDS-DMA, LPD steps ahead);
+//     only when they do not yet cover what it needs does wave 0 drain its
+//     queue and poll (bounded: on timeout *err is set and scores are invalid).
+// Every workgroup of the grid must be resident (host: use_lap_mode), so a
+// spinning consumer never blocks its producer.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void store16_sc1(void *gptr, uint4 v) {
   const u32x4 d = {v.x, v.y, v.z, v.w};
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(gptr), "v"(d) : "memory");
 }
+constexpr int ZRING = 16;  // z records resident in LDS (power of 2, >= lap_pd + 3)
 
 template <int M, int NW, bool F16, bool SOP>
 __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
-    const uint8_t *__restrict__ seqs, const int64_t *__restrict__ offs, int32_t G, int32_t YR,
-    int32_t lds_a, uint8_t *__restrict__ yf_base, int32_t *__restrict__ flags,
-    int32_t *__restrict__ err, int32_t *__restrict__ scores, PencilArgs pa) {
+    const uint8_t *__restrict__ seqs, const int64_t *__restrict__ offs, int32_t G, int32_t GZ,
+    int32_t YR, int32_t lds_a, uint8_t *__restrict__ yf_base, uint8_t *__restrict__ zf_base,
+    int32_t *__restrict__ flags, int32_t *__restrict__ err, int32_t *__restrict__ scores,
+    PencilArgs pa, unsigned long long *__restrict__ trace) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int PAIR_BYTES = 64 * REC_BYTES;
   constexpr int SLOT_BYTES = M * PAIR_BYTES;
   constexpr int ZT = 128 * M;
   constexpr int LPD = lap_pd(M);
+  // diagnostic trace (TSA_LAP_TRACE): per workgroup {start, loop begin, loop end, XCC id}
+  auto stamp = [&](int slot) {
+    if (trace != nullptr && threadIdx.x == 0) {
+      unsigned long long v;
+      if (slot == 3) {
+        unsigned x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        v = x;
+      }
+      else asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");
+      trace[(int64_t)blockIdx.x * 8 + slot] = v;
+    }
+  };
+  stamp(0);
+  stamp(3);
+  constexpr int ZREC = ((NW + 1) * 16 + 63) & ~63;  // z record: rows -1..NW-1 x 16 B
+  static_assert(ZRING >= LPD + 3, "z ring");
   uint8_t *xr = smem;                                    // [NW-1][2][M][64][16]
   uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT_BYTES;         // [LPD][M][64][16]
-  int32_t *fslot = (int32_t *)(xr0 + LPD * SLOT_BYTES);  // [LPD] prefetched producer flags
-  uint32_t *fin = (uint32_t *)(fslot + LPD);             // [M][64] final-step best
-  uint32_t *sA2 = fin + M * 64;                          // [la + lc + NW + ZT] A code pairs
+  uint8_t *zst = xr0 + LPD * SLOT_BYTES;                 // [4][ZREC] z staging (producer)
+  uint8_t *zring = zst + 4 * ZREC;                       // [ZRING][ZREC] z records (consumer)
+  // producer flags, LDS-DMA'd every step and read every step without a wait: the
+  // word holds whichever DMA landed last (flags only grow), a lower bound that
+  // lags by the DMA latency rather than by the prefetch distance
+  int32_t *fslot = (int32_t *)(zring + ZRING * ZREC);    // [1] y-producer flag
+  int32_t *zfslot = fslot + LPD;                         // [1] z-producer flag
+  uint32_t *fin = (uint32_t *)(zfslot + LPD);            // [M][64] final-step best
+  uint32_t *sA2 = fin + M * 64;                          // [la + ZT + NW + ZT] A code pairs
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -740,20 +800,26 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
   asm volatile("" : "+v"(Q), "+v"(fsv), "+v"(fpv));
   const PencilArgs pv = F16 ? pa : pin_score_consts(pa);
 
-  const int32_t tri = blockIdx.x / G, L = blockIdx.x % G;
+  const int32_t wg = blockIdx.x, q = wg % GZ, tri = wg / (G * GZ), L = (wg / GZ) % G;
   const int64_t o0 = offs[3 * (int64_t)tri], o1 = offs[3 * (int64_t)tri + 1];
   const int64_t o2 = offs[3 * (int64_t)tri + 2], o3 = offs[3 * (int64_t)tri + 3];
   const int32_t la = (int32_t)(o1 - o0), lb = (int32_t)(o2 - o1), lc = (int32_t)(o3 - o2);
-  const int32_t nlap = (lb + NW - 1) / NW;
-  if (L >= nlap) return;  // whole workgroup
-  const bool final_lap = L == nlap - 1;
-  const int32_t w_f = (lb - 1) % NW, k_f = lc - 1;
-  // steps of this lap; the final lap stops at the final cell (la, lb, lc)
-  const int32_t T = final_lap ? (la - 1) + w_f + k_f + 1 : la + (NW - 1) + (lc - 1);
-  uint8_t *yf_mine = yf_base + ((int64_t)tri * G + L) * YR * SLOT_BYTES;
-  const uint8_t *yf_prev = yf_mine - (int64_t)YR * SLOT_BYTES;
-  int32_t *flag_mine = flags + (int64_t)tri * G + L;
-  const int32_t *flag_prev = flag_mine - 1;
+  const int32_t nlap = (lb + NW - 1) / NW, ntile = (lc + ZT - 1) / ZT;
+  if (L >= nlap || q >= ntile) return;  // whole workgroup
+  const bool zin = q > 0, zout = q + 1 < ntile;
+  const int32_t zt_q = min(ZT, lc - q * ZT);  // positions of this tile
+  const bool final_wg = L == nlap - 1 && q == ntile - 1;
+  const int32_t w_f = (lb - 1) % NW, k_f = lc - 1 - q * ZT;
+  // steps of this workgroup; the final one stops at the final cell (la, lb, lc)
+  const int32_t T_full = la + (NW - 1) + (zt_q - 1);
+  const int32_t T = final_wg ? (la - 1) + w_f + k_f + 1 : T_full;
+  const int32_t T_zprev = la + (NW - 1) + (ZT - 1);  // steps of tile q-1 (full width)
+  uint8_t *yf_mine = yf_base + (int64_t)wg * YR * SLOT_BYTES;
+  const uint8_t *yf_prev = yf_mine - (int64_t)GZ * YR * SLOT_BYTES;  // (L-1, q)
+  uint8_t *zf_mine = zf_base + (int64_t)wg * YR * ZREC;
+  const uint8_t *zf_prev = zf_mine - (int64_t)YR * ZREC;             // (L, q-1)
+  int32_t *flag_mine = flags + wg;
+  const int32_t *flag_prev = flag_mine - GZ, *flag_zprev = flag_mine - 1;
 
   // A code pairs: entry j holds x = j-ZT (lo) and x = j-ZT-64 (hi), 0 outside [0, la)
   const int32_t na = lds_a / 4;
@@ -763,7 +829,6 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     const uint32_t c1 = (x1 >= 0 && x1 < la) ? SYM0 << (seqs[o0 + x1] & 3) : 0u;
     sA2[j] = c0 | (c1 << 16);
   }
-  __syncthreads();
   // position k of this wave is at x-1 = t - w - k: a[i] = sA2[t - w + ZT - lane - 128 i]
   const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
                           4u * (uint32_t)(ZT - w - lane - 128 * (M - 1));
@@ -775,11 +840,12 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
   {
     uint32_t one1 = 0x00010001u, sbcv = pa.h_sbc, kdv = pa.h_kd, k0v = pa.h_k0;
     asm volatile("" : "+v"(one1), "+v"(sbcv), "+v"(kdv), "+v"(k0v));
+    const int64_t oc = o2 + (int64_t)q * ZT;
 #pragma unroll
     for (int i = 0; i < M; ++i) {
       const int k0 = lane + 128 * i, k1 = lane + 64 + 128 * i;
-      const uint32_t c0 = k0 < lc ? SYM0 << (seqs[o2 + k0] & 3) : 0u;
-      const uint32_t c1 = k1 < lc ? SYM0 << (seqs[o2 + k1] & 3) : 0u;
+      const uint32_t c0 = k0 < zt_q ? SYM0 << (seqs[oc + k0] & 3) : 0u;
+      const uint32_t c1 = k1 < zt_q ? SYM0 << (seqs[oc + k1] & 3) : 0u;
       c[i] = c0 | (c1 << 16);
       b[i] = bw;  // one row per wave
       const uint32_t e01 = pk_eq1(bw, c[i], one1);
@@ -791,43 +857,68 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     }
   }
 
-  // wave 0 of lap L>0: row r of yf_prev feeds step r - (NW-1); prime LPD steps
-  int32_t seen = 0;  // rows of yf_prev known complete
-  auto ensure = [&](int32_t r) __attribute__((always_inline)) {  // row r must be published (r < the producer's T)
-    if (r < seen) return;
+  // ---- consumer side (wave 0): progress of the y and z producers
+  int32_t seen = 0, seen_z = 0;  // producer flags seen (rows < seen, z records < seen_z - 2)
+  uint32_t n_poll = 0, n_spin = 0;  // diagnostics (trace only)
+  auto poll = [&](const int32_t *fl, int32_t &sn, int32_t need) {  // until need < sn
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (uint32_t spin = 0;; ++spin) {
-      seen = __builtin_amdgcn_readfirstlane(
-          __hip_atomic_load(flag_prev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      if (r < seen) break;
+    ++n_poll;
+    for (uint32_t spin = 0;; ++spin, ++n_spin) {
+      sn = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (need < sn) break;
       if (spin > (1u << 22)) {
         if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        seen = 1 << 30;
+        sn = 1 << 30;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
   };
-  const int32_t T_prev = la + (NW - 1) + (lc - 1);  // rows lap L-1 publishes
-  auto fetch = [&](int32_t s2) __attribute__((always_inline)) {  // rows of step s2 -> xr0 slot s2 % LPD
+  const int32_t T_prev = T_full;  // rows lap L-1 publishes (same tile width)
+  auto fetch_y = [&](int32_t s2) {  // rows of step s2 -> xr0 slot s2 % LPD (+ flag word)
     const int32_t r = s2 + NW - 1;
-    if (r < T_prev) ensure(r);
+    if (r < T_prev && r >= seen) poll(flag_prev, seen, r);
     const int32_t rr = r < T_prev ? r : T_prev - 1;  // past the end: any valid row
 #pragma unroll
     for (int i = 0; i < M; ++i)
       dma16(yf_prev + ((int64_t)rr * M + i) * PAIR_BYTES + lane * REC_BYTES,
             xr0 + (s2 % LPD) * SLOT_BYTES + i * PAIR_BYTES);
-    if (lane == 0) dma4(flag_prev, fslot + (s2 % LPD));
+    if (lane == 0) dma4(flag_prev, fslot);
   };
-  if (w == 0 && L > 0)
-    for (int s2 = 0; s2 < LPD; ++s2) fetch(s2);
+  auto fetch_z = [&](int32_t i) {  // z record i -> zring (+ the flag word)
+#ifdef TSA_LAPZ_SYNC_DEBUG
+    if (i < T_zprev) { seen_z = 0; poll(flag_zprev, seen_z, i + 2); }
+#endif
+    if (i < T_zprev && i >= seen_z - 2) poll(flag_zprev, seen_z, i + 2);
+    const int32_t ii = i < T_zprev ? i : T_zprev - 1;
+    if (lane < ZREC / 16)
+      dma16(zf_prev + (int64_t)ii * ZREC + lane * 16, zring + (i & (ZRING - 1)) * ZREC);
+    if (lane == 0) dma4(flag_zprev, zfslot);
+  };
+  if (w == 0) {
+    // flag slots not DMA'd by the prologue must read as "nothing published"
+    if (lane < 2 * LPD) fslot[lane] = 0;  // fslot and zfslot
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // before any DMA lands there
+    if (L > 0)
+      for (int s2 = 0; s2 < LPD; ++s2) fetch_y(s2);
+    if (zin) {  // records ZT-1 .. ZT+LPD serve the first LPD+1 steps
+      for (int i = ZT - 1; i <= ZT + LPD; ++i) fetch_z(i);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      seen_z = max(seen_z, __builtin_amdgcn_readfirstlane(zfslot[0]));
+    }
+  }
+  __syncthreads();
+  stamp(1);
   const uint4 face = make_uint4(pa.f_single, pa.f_pair, pa.f_pair, 0u);
 
-  // ROLE 0: wave 0 of lap 0 (y = 0 face above); 1: wave 0 of a later lap (rows
-  // of lap L-1 via LDS-DMA); 2: middle waves; 3: the last wave (rows to global)
+  // ROLE (wave 0): bit 0 = rows of lap L-1 arrive (L > 0), bit 2 = z records of
+  // tile q-1 arrive (q > 0); 2 = middle waves; 3 = the last wave
   auto step = [&](auto ph, auto role, int32_t t) {
     constexpr int PH = decltype(ph)::value;
     constexpr int ROLE = decltype(role)::value;
+    constexpr bool W0 = ROLE == 0 || ROLE == 1 || ROLE == 4 || ROLE == 5;
+    constexpr bool YIN = ROLE == 1 || ROLE == 5, ZIN0 = ROLE == 4 || ROLE == 5;
     uint32_t a[M];
     {
       const uint32_t va = a_lane + 4u * (uint32_t)t;
@@ -837,17 +928,29 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
             va + 512u * (uint32_t)(M - 1 - i));
     }
     uint4 rec[M];
-    if constexpr (ROLE == 0) {
+    if constexpr (W0) {
+      // rows (+ flag) and the z record (+ flag) of step t were DMA'd LPD steps ago
+      constexpr int OPS = (YIN ? M + 1 : 0) + (ZIN0 ? 2 : 0);
+#ifdef TSA_LAPZ_SYNC_DEBUG
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      if constexpr (OPS > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS * (LPD - 1)) : "memory");
+      if constexpr (YIN) {
+        const uint8_t *src = xr0 + (t % LPD) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
-      for (int i = 0; i < M; ++i) rec[i] = face;
-    } else if constexpr (ROLE == 1) {
-      // rows + flag of step t were DMA'd LPD steps ago: M+1 ops per step
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((M + 1) * (LPD - 1)) : "memory");
-      const uint8_t *src = xr0 + (t % LPD) * SLOT_BYTES + lane * REC_BYTES;
+        for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
+        // producer progress as of the last landed flag DMA (no wait, no round trip)
+        seen = max(seen, __builtin_amdgcn_readfirstlane(
+                             *(volatile const __attribute__((address_space(3))) int32_t *)(
+                                 const __attribute__((address_space(3))) void *)fslot));
+      } else {
 #pragma unroll
-      for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
-      // producer progress as of ~LPD steps ago, free of any round trip
-      seen = max(seen, __builtin_amdgcn_readfirstlane(fslot[t % LPD]));
+        for (int i = 0; i < M; ++i) rec[i] = face;  // y = 0 face
+      }
+      if constexpr (ZIN0)
+        seen_z = max(seen_z, __builtin_amdgcn_readfirstlane(
+                                 *(volatile const __attribute__((address_space(3))) int32_t *)(
+                                     const __attribute__((address_space(3))) void *)zfslot));
     } else {
       const uint8_t *src = xr + ((w - 1) * 2 + (PH ^ 1)) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
@@ -891,9 +994,18 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
                                     nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    if (final_lap && t == T - 1 && w == w_f) {
+    if (final_wg && t == T - 1 && w == w_f) {
 #pragma unroll
       for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
+    }
+    // z staging: this wave's last position, and (wave 0) the row above's
+    if (zout && lane == 63) {
+      lds_write16(zst + (t & 3) * ZREC + (w + 1) * 16,
+                  make_uint4(oIz[M - 1], oIxz[M - 1], oIyz[M - 1], oBest[M - 1]));
+      if constexpr (W0) {  // rec of step t = the row above at step t-1
+        if (t >= 1)
+          lds_write16(zst + ((t - 1) & 3) * ZREC, make_uint4(0u, 0u, rec[M - 1].z, rec[M - 1].w));
+      }
     }
     if constexpr (ROLE != 3) {
       uint8_t *dst = xr + (w * 2 + PH) * SLOT_BYTES + lane * REC_BYTES;
@@ -905,6 +1017,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
       for (int i = 0; i < M; ++i)
         store16_sc1(yf_mine + ((int64_t)t * M + i) * PAIR_BYTES + lane * REC_BYTES,
                     make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
+      if (zout && t >= 2 && lane <= NW) {  // z record of step t-2 is complete in LDS
+        const uint4 v = lds_read16(zst + ((t - 2) & 3) * ZREC + lane * 16);
+        store16_sc1(zf_mine + (int64_t)(t - 2) * ZREC + lane * 16, v);
+      }
     }
 #pragma unroll
     for (int i = 0; i < M; ++i) {
@@ -914,15 +1030,34 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     uint32_t rz[M], rw[M];
 #pragma unroll
     for (int i = 0; i < M; ++i) { rz[i] = rec[i].z; rw[i] = rec[i].w; }
-    zshift<M>(shIxz[PH], oIxz, sel, pa.f_pair);  // z = 0 face for position 0
-    zshift<M>(shIz, oIz, sel, pa.f_single);
-    zshift<M>(svIyz, rz, sel, pa.f_pair);
-    zshift<M>(svM[PH], rw, sel, 0u);
-    if constexpr (ROLE == 1) fetch(t + LPD);  // usually covered by the prefetched flag
+    // position 0's z-1 neighbour: the z = 0 face, or tile q-1's last position
+    uint32_t fIxz = pa.f_pair, fIz = pa.f_single, fIyz = pa.f_pair, fM = 0u;
+    if (zin) {
+      const uint8_t *ra = zring + ((t + ZT) & (ZRING - 1)) * ZREC + (w + 1) * 16;
+      const uint8_t *rb = zring + ((t + ZT - 1) & (ZRING - 1)) * ZREC + w * 16 + 8;
+      typedef unsigned u32x2_lds __attribute__((ext_vector_type(2)));
+      const u32x2_lds za = *(const __attribute__((address_space(3))) u32x2_lds *)(
+          const __attribute__((address_space(3))) void *)ra;
+      const u32x2_lds zb = *(const __attribute__((address_space(3))) u32x2_lds *)(
+          const __attribute__((address_space(3))) void *)rb;
+      fIz = za.x;
+      fIxz = za.y;
+      fIyz = zb.x;
+      fM = zb.y;
+    }
+    zshift<M>(shIxz[PH], oIxz, sel, fIxz);
+    zshift<M>(shIz, oIz, sel, fIz);
+    zshift<M>(svIyz, rz, sel, fIyz);
+    zshift<M>(svM[PH], rw, sel, fM);
+    if constexpr (W0) {
+      if constexpr (YIN) fetch_y(t + LPD);  // usually covered by the prefetched flag
+      if constexpr (ZIN0) fetch_z(t + ZT + LPD + 1);
+    }
     if constexpr (ROLE == 3) {
-      // rows <= t - LAP_SLACK complete (M stores + 1 flag store per step)
+      // rows <= t - LAP_SLACK (z records two steps older) complete: per step M row
+      // stores, 1 flag store and at most one z store -- the count assumes none,
+      // so with a z store it waits for slightly more than it needs
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LAP_SLACK * (M + 1)) : "memory");
-      // exactly M + 1 vector-memory ops per step keep that count exact
       if (lane == 0)
         __hip_atomic_store(flag_mine, t >= LAP_SLACK ? t - LAP_SLACK + 1 : 0,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -939,20 +1074,36 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     if (t < T) TSA_INLINE_IF_WIDE(step(std::integral_constant<int, 0>{}, role, t));
   };
   if (w == 0) {
-    if (L == 0) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 0>{}));
-    else TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 1>{}));
+    if (L == 0) {
+      if (zin) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 4>{}));
+      else TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 0>{}));
+    } else {
+      if (zin) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 5>{}));
+      else TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 1>{}));
+    }
   } else if (w == NW - 1) {
     TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 3>{}));
   } else {
     TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 2>{}));
   }
+  stamp(2);
+  if (trace != nullptr && threadIdx.x == 0) {
+    trace[(int64_t)blockIdx.x * 8 + 4] = n_poll;
+    trace[(int64_t)blockIdx.x * 8 + 5] = n_spin;
+  }
+  // the last two z records: every wave's staging writes are done after this barrier
+  __syncthreads();
   if (w == NW - 1) {
+    if (zout && lane <= NW)
+      for (int32_t s2 = max(T - 2, 0); s2 < T; ++s2)
+        store16_sc1(zf_mine + (int64_t)s2 * ZREC + lane * 16,
+                    lds_read16(zst + (s2 & 3) * ZREC + lane * 16));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(flag_mine, T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0)
+      __hip_atomic_store(flag_mine, T + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (final_lap) {
-    __syncthreads();
+  if (final_wg) {
     if (threadIdx.x == 0) {
       const int32_t l_f = k_f & 63, i_f = k_f >> 7, h_f = (k_f >> 6) & 1;
       const uint32_t v = fin[i_f * 64 + l_f];
@@ -1049,20 +1200,41 @@ static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
 
 template <int M, int NW, bool F16, bool SOP>
 static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, int32_t max_la,
-                      int32_t max_lc, const LapGeom &g, int32_t *d_scores, void *d_ws,
-                      const PencilArgs &pa, hipStream_t stream) {
-  const int32_t lds_a = 4 * ((max_la + max_lc + NW + 128 * M + 3) & ~3);
-  const size_t lds = lap_lds(M, NW, max_la, max_lc);
+                      const LapGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
+                      hipStream_t stream) {
+  const int32_t lds_a = 4 * ((max_la + NW + 2 * 128 * M + 3) & ~3);
   auto kfn = pencil_lap_kernel<M, NW, F16, SOP>;
-  if (lds > LDS_MAX) return TSA_EINVAL;
+  if (g.lds > LDS_MAX) return TSA_EINVAL;
   if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
+                          (int)g.lds) != hipSuccess)
     return TSA_EDEVICE;
-  int32_t *flags = (int32_t *)d_ws;           // [n*G] progress + [1] error word
+  const int64_t wgs = (int64_t)n * g.G * g.GZ;
+  int32_t *flags = (int32_t *)d_ws;  // [wgs] progress + [1] error word
   if (hipMemsetAsync(flags, 0, g.flag_bytes, stream) != hipSuccess) return TSA_EDEVICE;
   uint8_t *yf = (uint8_t *)d_ws + g.flag_bytes;
-  hipLaunchKernelGGL(kfn, dim3(n * g.G), dim3(64 * NW), lds, stream, d_seqs, d_offsets, g.G, g.YR,
-                     lds_a, yf, flags, flags + (size_t)n * g.G, d_scores, pa);
+  uint8_t *zf = yf + g.yf_bytes;
+  unsigned long long *trace = nullptr;
+  const char *tpath = getenv("TSA_LAP_TRACE");  // diagnostic: per-WG timestamps to a CSV file
+  if (tpath && hipMalloc(&trace, (size_t)wgs * 8 * 8) != hipSuccess) return TSA_ENOMEM;
+  if (trace && hipMemsetAsync(trace, 0, (size_t)wgs * 8 * 8, stream) != hipSuccess) return TSA_EDEVICE;
+  hipLaunchKernelGGL(kfn, dim3((uint32_t)wgs), dim3(64 * NW), g.lds, stream, d_seqs, d_offsets,
+                     g.G, g.GZ, g.YR, lds_a, yf, zf, flags, flags + wgs, d_scores, pa, trace);
+  if (trace) {
+    std::vector<unsigned long long> h((size_t)wgs * 8);
+    if (hipMemcpyAsync(h.data(), trace, h.size() * 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+      return TSA_EDEVICE;
+    (void)hipFree(trace);
+    if (FILE *fp = fopen(tpath, "w")) {
+      fprintf(fp, "wg,tri,lap,tile,start,loop_begin,loop_end,xcc,polls,spins\n");
+      for (int64_t i = 0; i < wgs; ++i)
+        fprintf(fp, "%lld,%lld,%lld,%lld,%llu,%llu,%llu,%llu,%llu,%llu\n", (long long)i,
+                (long long)(i / ((int64_t)g.G * g.GZ)), (long long)((i / g.GZ) % g.G),
+                (long long)(i % g.GZ), h[i * 8], h[i * 8 + 1], h[i * 8 + 2], h[i * 8 + 3],
+                h[i * 8 + 4], h[i * 8 + 5]);
+      fclose(fp);
+    }
+  }
   return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
 }
 
@@ -1092,9 +1264,9 @@ int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t
   const bool sop = pa.sop != 0;
   if (use_lap_mode(n, max_la, max_lb, max_lc)) {
     const LapGeom lg = lap_geom(n, max_la, max_lb, max_lc);
-    if (ws_bytes < lg.flag_bytes + lg.yf_bytes) return TSA_ENOMEM;
-    return TSA_SHAPES(launch_lap, lg.M, lg.NW, f16, sop, d_seqs, d_offsets, n, max_la, max_lc,
-                      lg, d_scores, d_ws, pa, stream);
+    if (ws_bytes < lg.flag_bytes + lg.yf_bytes + lg.zf_bytes) return TSA_ENOMEM;
+    return TSA_SHAPES(launch_lap, lg.M, lg.NW, f16, sop, d_seqs, d_offsets, n, max_la, lg,
+                      d_scores, d_ws, pa, stream);
   }
   const PencilGeom g = pencil_geom(max_la, max_lc);
   const int32_t grid = n < 65535 ? n : 65535;

@@ -226,6 +226,25 @@ def test_pencil_lap_rows_per_lap(gpu, orc, synth, monkeypatch, nw):
         assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (nw, la, lb, lc)
 
 
+@pytest.mark.parametrize("zt", ["128", "256", "512"])
+def test_pencil_lap_z_tiles(gpu, orc, monkeypatch, zt):
+    # single-cube lap kernel with the z axis cut into 128*M-position tiles that
+    # hand their last position to the next tile's position 0 every step;
+    # partial last tiles, one-lap cubes, LA below/above the tile width
+    monkeypatch.setenv("TSA_LAP_ZT", zt)
+    rng = np.random.default_rng(60 + int(zt))
+    p, op = gpu.TsaParams.default(score_bits=16), orc.default_params(score_bits=16)
+    for la, lb, lc in [(300, 16, 300), (130, 40, 260), (150, 16, 129), (64, 17, 130),
+                       (256, 48, 256), (40, 33, 513), (520, 20, 700)]:
+        a = rng.integers(0, 4, max(la, lc)).astype(np.uint8)
+        b = a[:lb].copy()
+        b[::5] = (b[::5] + 1) % 4
+        c = a[:lc].copy()
+        c[::9] = (c[::9] + 2) % 4  # related sequences: long matching runs
+        assert gpu.score(a[:la], b, c, p, kernel="pencil") == orc.score(a[:la], b, c, op), \
+            (zt, la, lb, lc)
+
+
 def test_pencil_lap_mode_small_batch(gpu, orc):
     # several triples in lap mode at once (n * laps <= resident workgroups)
     rng = np.random.default_rng(9)
