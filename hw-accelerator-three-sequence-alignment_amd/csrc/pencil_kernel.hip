@@ -57,7 +57,7 @@ __host__ __device__ constexpr int helix_pd(int M) { return M >= 8 ? 2 : M >= 4 ?
 #define TSA_LAP_PD 4
 #endif
 #ifndef TSA_LAP_SLACK
-#define TSA_LAP_SLACK 4
+#define TSA_LAP_SLACK 2
 #endif
 #ifndef TSA_LAP_PD1  // M = 1: short steps, so more steps must cover the DMA latency
 #define TSA_LAP_PD1 TSA_LAP_PD
@@ -860,25 +860,29 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
   // ---- consumer side (wave 0): progress of the y and z producers
   int32_t seen = 0, seen_z = 0;  // producer flags seen (rows < seen, z records < seen_z - 2)
   uint32_t n_poll = 0, n_spin = 0;  // diagnostics (trace only)
-  auto poll = [&](const int32_t *fl, int32_t &sn, int32_t need) {  // until need < sn
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // Wait until need < producer flag, reading the flag through its LDS word and
+  // refreshing that word by LDS-DMA: no vmcnt drain, so the row and record DMAs
+  // already in flight keep going (a drained poll cost ~2-4 us each)
+  auto poll = [&](const int32_t *fl, int32_t *word, int32_t &sn, int32_t need) {
     ++n_poll;
     for (uint32_t spin = 0;; ++spin, ++n_spin) {
-      sn = __builtin_amdgcn_readfirstlane(
-          __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      sn = max(sn, __builtin_amdgcn_readfirstlane(
+                       *(volatile const __attribute__((address_space(3))) int32_t *)(
+                           const __attribute__((address_space(3))) void *)word));
       if (need < sn) break;
       if (spin > (1u << 22)) {
         if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sn = 1 << 30;
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
+      if ((spin & 15) == 0 && lane == 0) dma4(fl, word);
+      __builtin_amdgcn_s_sleep(2);
     }
   };
   const int32_t T_prev = T_full;  // rows lap L-1 publishes (same tile width)
   auto fetch_y = [&](int32_t s2) {  // rows of step s2 -> xr0 slot s2 % LPD (+ flag word)
     const int32_t r = s2 + NW - 1;
-    if (r < T_prev && r >= seen) poll(flag_prev, seen, r);
+    if (r < T_prev && r >= seen) poll(flag_prev, fslot, seen, r);
     const int32_t rr = r < T_prev ? r : T_prev - 1;  // past the end: any valid row
 #pragma unroll
     for (int i = 0; i < M; ++i)
@@ -887,10 +891,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     if (lane == 0) dma4(flag_prev, fslot);
   };
   auto fetch_z = [&](int32_t i) {  // z record i -> zring (+ the flag word)
-#ifdef TSA_LAPZ_SYNC_DEBUG
-    if (i < T_zprev) { seen_z = 0; poll(flag_zprev, seen_z, i + 2); }
-#endif
-    if (i < T_zprev && i >= seen_z - 2) poll(flag_zprev, seen_z, i + 2);
+    if (i < T_zprev && i >= seen_z - 2) poll(flag_zprev, zfslot, seen_z, i + 2);
     const int32_t ii = i < T_zprev ? i : T_zprev - 1;
     if (lane < ZREC / 16)
       dma16(zf_prev + (int64_t)ii * ZREC + lane * 16, zring + (i & (ZRING - 1)) * ZREC);
@@ -931,9 +932,6 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     if constexpr (W0) {
       // rows (+ flag) and the z record (+ flag) of step t were DMA'd LPD steps ago
       constexpr int OPS = (YIN ? M + 1 : 0) + (ZIN0 ? 2 : 0);
-#ifdef TSA_LAPZ_SYNC_DEBUG
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
       if constexpr (OPS > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS * (LPD - 1)) : "memory");
       if constexpr (YIN) {
         const uint8_t *src = xr0 + (t % LPD) * SLOT_BYTES + lane * REC_BYTES;
