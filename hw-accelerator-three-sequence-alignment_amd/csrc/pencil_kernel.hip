@@ -57,10 +57,10 @@ __host__ __device__ constexpr int helix_pd(int M) { return M >= 8 ? 2 : M >= 4 ?
 #define TSA_LAP_PD 4
 #endif
 #ifndef TSA_LAP_SLACK
-#define TSA_LAP_SLACK 2
+#define TSA_LAP_SLACK 1
 #endif
-#ifndef TSA_LAP_PD1  // M = 1: short steps, so more steps must cover the DMA latency
-#define TSA_LAP_PD1 TSA_LAP_PD
+#ifndef TSA_LAP_PD1  // M = 1 (measured: 3 beats 2, 4, 6, 8 and 12 at 256^3 and 1024^3)
+#define TSA_LAP_PD1 3
 #endif
 __host__ __device__ constexpr int lap_pd(int M) {
   return M >= 8 ? (TSA_LAP_PD < 3 ? TSA_LAP_PD : 3) : M == 1 ? TSA_LAP_PD1 : TSA_LAP_PD;
