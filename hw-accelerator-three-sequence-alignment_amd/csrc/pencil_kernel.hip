@@ -148,7 +148,8 @@ static int lap_waves_per_cu(int M) { return M == 1 ? 32 : M == 2 ? 16 : 8; }
 struct LapGeom {
   int32_t M, NW, G, GZ, YR;
   size_t lds, zrec, yf_bytes, zf_bytes, flag_bytes;
-  bool ok;
+  int64_t waves;  // grid / resident slots: 1 = every workgroup resident at once
+  bool ok;        // feasible (LDS) and more than one workgroup per triple
 };
 static LapGeom lap_geom_m(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M) {
   LapGeom g;
@@ -165,37 +166,73 @@ static LapGeom lap_geom_m(int32_t n, int32_t max_la, int32_t max_lb, int32_t max
   g.flag_bytes = ((wgs + 1) * sizeof(int32_t) + 255) & ~(size_t)255;
   const int64_t per_cu =
       g.lds > LDS_MAX ? 0 : std::min<int64_t>(LDS_MAX / g.lds, lap_waves_per_cu(M) / g.NW);
-  // every workgroup resident, and at least two laps or tiles to overlap
-  g.ok = (int64_t)wgs <= 256 * per_cu && (g.G >= 2 || g.GZ >= 2);
+  g.waves = per_cu > 0 ? ((int64_t)wgs + 256 * per_cu - 1) / (256 * per_cu) : 0;
+  g.ok = per_cu > 0 && (g.G >= 2 || g.GZ >= 2);
   return g;
-}
-// The narrowest z-tile (128*M positions) whose grid fits; TSA_LAP_ZT forces one.
-static LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
-  const int m_lc = pencil_pairs(max_lc);  // one tile covers all of LC
-  if (const char *e = getenv("TSA_LAP_ZT")) {
-    const int zt = atoi(e);
-    const int M = zt <= 128 ? 1 : zt <= 256 ? 2 : zt <= 512 ? 4 : 8;
-    return lap_geom_m(n, max_la, max_lb, max_lc, std::min(M, m_lc));
-  }
-  LapGeom g = lap_geom_m(n, max_la, max_lb, max_lc, 1);
-  for (int M = 2; !g.ok && M <= m_lc; M *= 2) g = lap_geom_m(n, max_la, max_lb, max_lc, M);
-  return g;
-}
-static bool use_lap_mode(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
-  if (const char *e = getenv("TSA_PENCIL_MODE")) {
-    if (!strcmp(e, "helix")) return false;
-  }
-  return lap_geom(n, max_la, max_lb, max_lc).ok;
 }
 
-size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+// Cost model for the mode choice, in M = 2 step units. Measured single-workgroup
+// step times: 0.56 us (M = 1), 0.88 us (M = 2); a lap or tile hand-off adds
+// ~LAP_LAG steps of flag and DMA latency to the chain.
+static double step_cost(int M) { return M == 1 ? 0.62 : M == 2 ? 1.0 : M == 4 ? 1.7 : 3.4; }
+constexpr int LAP_LAG = 30;
+// A grid beyond the resident slots runs in dispatch waves that barely overlap
+// (a triple's later laps wait for slots its earlier laps free): calibrated at
+// 256^3, 32 triples 3.0 ms vs helix 6.0 ms, 64 triples 6.2 vs 5.3 ms, so each
+// wave costs ~2.8x its chain and streaming is limited to a few waves.
+constexpr int64_t LAP_MAX_WAVES = 3;
+static double lap_est(const LapGeom &g, int32_t max_la) {
+  const double T = max_la + g.NW + 128 * g.M;
+  const double chain = (double)(g.G - 1) * (g.NW + LAP_LAG) + (double)(g.GZ - 1) * (128 * g.M + LAP_LAG);
+  return (g.waves <= 1 ? chain + T : 2.8 * g.waves * (chain + T)) * step_cost(g.M);
+}
+static double helix_est(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  const PencilGeom g = pencil_geom(max_la, max_lc);
+  const int nw = helix_nw(g.M);
+  const int64_t per_cu = std::max<int64_t>(
+      1, std::min<int64_t>(LDS_MAX / helix_lds(g.M, nw, g.P, max_lb), waves_per_cu(g.M) / nw));
+  const double T = (double)((max_lb - 1) / nw) * g.P + max_la + nw + max_lc;
+  return (double)((n + 256 * per_cu - 1) / (256 * per_cu)) * T * step_cost(g.M);
+}
+
+// The lap kernel's geometry if it should run, else .ok = false (helix).
+// Resident grids (waves == 1) are always safe: a spinning consumer never blocks
+// its producer. With stream_ok the grid may exceed the resident slots: producers
+// always have lower block indices than their consumers, so with blocks dispatched
+// in order (observed, not promised by HIP) a consumer's producer is running or
+// done; spins are bounded and the caller checks the error word and falls back.
+static LapGeom lap_choice(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
+                          bool stream_ok) {
+  LapGeom none;
+  none.ok = false;
+  const char *mode = getenv("TSA_PENCIL_MODE");
+  if (mode && !strcmp(mode, "helix")) return none;
+  const bool force = mode && !strcmp(mode, "lap");
+  const int m_lc = pencil_pairs(max_lc);  // one tile covers all of LC
+  int m_lo = 1, m_hi = m_lc;
+  if (const char *e = getenv("TSA_LAP_ZT")) {  // tuning knob: force the tile width
+    const int zt = atoi(e);
+    m_lo = m_hi = std::min(zt <= 128 ? 1 : zt <= 256 ? 2 : zt <= 512 ? 4 : 8, m_lc);
+  }
+  LapGeom best = none;
+  double best_est = 0;
+  for (int M = m_lo; M <= m_hi; M *= 2) {
+    const LapGeom g = lap_geom_m(n, max_la, max_lb, max_lc, M);
+    if (!g.ok || (g.waves > 1 && !stream_ok) || g.waves > LAP_MAX_WAVES) continue;
+    const double e = lap_est(g, max_la);
+    if (!best.ok || e < best_est) { best = g; best_est = e; }
+  }
+  if (best.ok && !force && best_est >= helix_est(n, max_la, max_lb, max_lc)) return none;
+  return best;
+}
+
+size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
+                              bool stream_ok) {
   if (!pencil_shape_ok(max_la, max_lb, max_lc)) return 0;
   const size_t helix = (size_t)std::min<int32_t>(n, 65535) *
                        (size_t)pencil_geom(max_la, max_lc).ring_bytes_per_triple;
-  if (use_lap_mode(n, max_la, max_lb, max_lc)) {
-    const LapGeom g = lap_geom(n, max_la, max_lb, max_lc);
-    return std::max(helix, g.flag_bytes + g.yf_bytes + g.zf_bytes);
-  }
+  const LapGeom g = lap_choice(n, max_la, max_lb, max_lc, stream_ok);
+  if (g.ok) return std::max(helix, g.flag_bytes + g.yf_bytes + g.zf_bytes);
   return helix;
 }
 
@@ -744,8 +781,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 //   consumer: the flag words travel with the data (LDS-DMA, LPD steps ahead);
 //     only when they do not yet cover what it needs does wave 0 drain its
 //     queue and poll (bounded: on timeout *err is set and scores are invalid).
-// Every workgroup of the grid must be resident (host: use_lap_mode), so a
-// spinning consumer never blocks its producer.
+// Producers have lower block indices than their consumers; the host keeps the
+// grid resident or relies on in-order dispatch (lap_choice), so a spinning
+// consumer never blocks its producer.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void store16_sc1(void *gptr, uint4 v) {
   const u32x4 d = {v.x, v.y, v.z, v.w};
@@ -1254,15 +1292,17 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
 int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                         int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
                         const Range &bound, int32_t *d_scores, void *d_ws, size_t ws_bytes,
-                        hipStream_t stream) {
+                        hipStream_t stream, bool stream_ok, int32_t **d_err) {
+  if (d_err) *d_err = nullptr;
   if (n <= 0) return TSA_OK;
   if (!pencil_shape_ok(max_la, max_lb, max_lc)) return TSA_EINVAL;
   const bool f16 = use_f16(kp, bound);
   const PencilArgs pa = make_args(kp, f16);
   const bool sop = pa.sop != 0;
-  if (use_lap_mode(n, max_la, max_lb, max_lc)) {
-    const LapGeom lg = lap_geom(n, max_la, max_lb, max_lc);
+  const LapGeom lg = lap_choice(n, max_la, max_lb, max_lc, stream_ok);
+  if (lg.ok) {
     if (ws_bytes < lg.flag_bytes + lg.yf_bytes + lg.zf_bytes) return TSA_ENOMEM;
+    if (d_err) *d_err = (int32_t *)d_ws + (size_t)n * lg.G * lg.GZ;
     return TSA_SHAPES(launch_lap, lg.M, lg.NW, f16, sop, d_seqs, d_offsets, n, max_la, lg,
                       d_scores, d_ws, pa, stream);
   }

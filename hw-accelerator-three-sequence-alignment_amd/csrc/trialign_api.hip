@@ -184,15 +184,17 @@ static int choose_kernel(int32_t kernel, const tsa_params *p, int64_t la, int64_
   return ok ? TSA_KERNEL_PENCIL : TSA_KERNEL_PLANE;
 }
 
-static size_t workspace_for(int kind, int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+// stream_ok: only the synchronous paths, which check the lap kernel's error word
+static size_t workspace_for(int kind, int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
+                            bool stream_ok = false) {
   if (kind == TSA_KERNEL_PLANE) return plane_workspace_bytes(n, max_la, max_lb, max_lc);
-  return pencil_workspace_bytes(n, max_la, max_lb, max_lc);
+  return pencil_workspace_bytes(n, max_la, max_lb, max_lc, stream_ok);
 }
 
 static int launch_kind(int kind, const uint8_t *d_seqs, const int64_t *d_off, int32_t n,
                        int32_t max_la, int32_t max_lb, int32_t max_lc, const tsa_params *p,
                        int32_t *d_scores, int32_t *d_final7, void *ws, size_t ws_bytes,
-                       hipStream_t s) {
+                       hipStream_t s, bool stream_ok = false, int32_t **d_err = nullptr) {
   KParams kp;
   int rc = build_kparams(p, &kp);
   if (rc) return rc;
@@ -200,7 +202,8 @@ static int launch_kind(int kind, const uint8_t *d_seqs, const int64_t *d_off, in
     return plane_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp, d_scores, d_final7,
                               ws, ws_bytes, s);
   return pencil_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp,
-                             value_bound(p, max_la, max_lb, max_lc), d_scores, ws, ws_bytes, s);
+                             value_bound(p, max_la, max_lb, max_lc), d_scores, ws, ws_bytes, s,
+                             stream_ok, d_err);
 }
 
 #define HIPCHK(x)                                   \
@@ -224,10 +227,14 @@ static int run_host_batch_on_device(int device, const uint8_t *seqs, const int64
   }
   const int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
   if (kind < 0) return TSA_ERANGE;
-  // chunk so the workspace stays under ~8 GiB and grid.z under 65535
-  const size_t per = workspace_for(kind, 1, max_la, max_lb, max_lc);
+  // chunk so the workspace stays under ~8 GiB and grid.z under 65535; the
+  // workspace is what the chunk's plan (or its fallback) needs
+  const size_t per = std::max(workspace_for(kind, 1, max_la, max_lb, max_lc, true),
+                              workspace_for(kind, 1, max_la, max_lb, max_lc, false));
   int32_t chunk = (int32_t)std::max<size_t>(1, std::min<size_t>((size_t)8 << 30, (size_t)n * per) / per);
   chunk = std::min(chunk, std::min(n, 65535));
+  const size_t ws_bytes = std::max(workspace_for(kind, chunk, max_la, max_lb, max_lc, true),
+                                   workspace_for(kind, chunk, max_la, max_lb, max_lc, false));
   const int64_t base = offsets[3 * (int64_t)i0];
   const int64_t nbytes = offsets[3 * (int64_t)i1] - base;
   uint8_t *d_seqs = nullptr;
@@ -243,18 +250,27 @@ static int run_host_batch_on_device(int device, const uint8_t *seqs, const int64
       hipMalloc(&d_off, off.size() * sizeof(int64_t)) != hipSuccess ||
       hipMalloc(&d_scores, (size_t)n * sizeof(int32_t)) != hipSuccess ||
       (final7 && hipMalloc(&d_final, (size_t)n * 7 * sizeof(int32_t)) != hipSuccess) ||
-      hipMalloc(&d_ws, (size_t)chunk * per) != hipSuccess) {
+      hipMalloc(&d_ws, std::max<size_t>(ws_bytes, 16)) != hipSuccess) {
     rc = TSA_ENOMEM;
     goto done;
   }
   HIPCHK(hipMemcpyAsync(d_seqs, seqs + base, nbytes, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(d_off, off.data(), off.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemsetAsync(d_ws, 0, (size_t)chunk * per, s));
+  HIPCHK(hipMemsetAsync(d_ws, 0, ws_bytes, s));
   for (int32_t c0 = 0; c0 < n && rc == TSA_OK; c0 += chunk) {
     const int32_t cn = std::min(chunk, n - c0);
+    int32_t *d_err = nullptr;
     rc = launch_kind(kind, d_seqs, d_off + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p,
                      d_scores + c0, d_final ? d_final + 7 * (int64_t)c0 : nullptr, d_ws,
-                     (size_t)chunk * per, s);
+                     ws_bytes, s, true, &d_err);
+    if (rc == TSA_OK && d_err) {  // lap kernel: a timed-out hand-off invalidates the chunk
+      int32_t herr = 0;
+      HIPCHK(hipMemcpyAsync(&herr, d_err, sizeof(herr), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      if (herr)
+        rc = launch_kind(kind, d_seqs, d_off + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p,
+                         d_scores + c0, nullptr, d_ws, ws_bytes, s, false, nullptr);
+    }
   }
   if (rc) goto done;
   HIPCHK(hipMemcpyAsync(scores + i0, d_scores, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, s));

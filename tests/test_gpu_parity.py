@@ -255,6 +255,26 @@ def test_pencil_lap_mode_small_batch(gpu, orc):
     assert np.array_equal(got, orc.score_batch(seqs, offs, nthreads=8))
 
 
+def test_pencil_lap_streaming_batch(gpu, orc, monkeypatch, tmp_path):
+    # sync batch API with more lap workgroups than resident slots: the grid runs
+    # in 2-3 dispatch waves (bounded spins, error word checked, helix rerun on
+    # timeout); 100 triples x 8 laps = 800 workgroups for 512 slots. The lap
+    # trace proves the streaming grid ran.
+    monkeypatch.setenv("TSA_PENCIL_MODE", "lap")
+    trace = tmp_path / "lap.csv"
+    monkeypatch.setenv("TSA_LAP_TRACE", str(trace))
+    rng = np.random.default_rng(91)
+    triples = []
+    for _ in range(100):
+        la, lc = int(rng.integers(100, 129)), int(rng.integers(1, 129))
+        triples.append(tuple(rng.integers(0, 4, n).astype(np.uint8) for n in (la, 128, lc)))
+    seqs, offs = gpu.pack_batch(triples)
+    assert np.array_equal(gpu.score_batch(triples),
+                          orc.score_batch(seqs, offs, nthreads=8))
+    rows = trace.read_text().splitlines()
+    assert len(rows) - 1 == 800
+
+
 def test_pencil_ragged_batch(gpu, orc):
     rng = np.random.default_rng(77)
     triples = []
