@@ -115,7 +115,9 @@ static size_t helix_lds(int M, int NW, int32_t P, int32_t max_lb) {
          4 * ((size_t)P + 128 * M) + 4 * (((size_t)max_lb + 3) & ~(size_t)3) + (size_t)M * 256;
 }
 
-bool pencil_supported(const tsa_params *p) { return p != nullptr; }
+// The factored messages widen each target's highest-penalty group to all seven
+// states, exact only when gap_open >= gap_extend (cell_messages_f16).
+bool pencil_supported(const tsa_params *p) { return p != nullptr && p->gap_open >= p->gap_extend; }
 
 static bool pencil_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc) {
   if (!(max_la >= 1 && max_la <= MAX_LA && max_lb >= 1 && max_lb <= MAX_LB && max_lc >= 1 &&
@@ -359,22 +361,20 @@ __device__ __forceinline__ void cell_messages(
     const uint32_t A1 = pk_max(pYZ, qXY_XZ);  // Ix  <- {Iy,Iz,Ixy,Ixz} at GO+GE
     const uint32_t A2 = pk_max(pXZ, qXY_YZ);  // Iy  <- {Ix,Iz,Ixy,Iyz}
     const uint32_t A3 = pk_max(pXY, qYZ_XZ);  // Iz  <- {Ix,Iy,Iyz,Ixz}
-    const uint32_t B1 = pk_max(sM, sYZ);      // Ix  <- {M,Iyz} at 2GO
-    const uint32_t B2 = pk_max(sM, sXZ);      // Iy  <- {M,Ixz}
-    const uint32_t B3 = pk_max(sM, sXY);      // Iz  <- {M,Ixy}
     const uint32_t C1 = pk_max(pXY, sXY);     // Ixy <- {Ix,Iy,Ixy} at GE
     const uint32_t C2 = pk_max(pYZ, sYZ);     // Iyz <- {Iy,Iz,Iyz}
     const uint32_t C3 = pk_max(pXZ, sXZ);     // Ixz <- {Ix,Iz,Ixz}
-    const uint32_t D1 = pk_max(B1, pk_max(sZ, sXZ));  // Ixy <- {M,Iz,Iyz,Ixz} at GO
-    const uint32_t D2 = pk_max(B2, pk_max(sX, sXY));  // Iyz <- {M,Ix,Ixy,Ixz}
-    const uint32_t D3 = pk_max(B3, pk_max(sY, sYZ));  // Ixz <- {M,Iy,Ixy,Iyz}
-    oBest[i] = pk_max(pk_max(A1, B1), sX);            // MAX7 of the states
-    nIx[i] = pk_max(pk_max(pk_sub(sX, pa.E2), pk_sub(A1, pa.OE)), pk_sub(B1, pa.O2));
-    oIy[i] = pk_max(pk_max(pk_sub(sY, pa.E2), pk_sub(A2, pa.OE)), pk_sub(B2, pa.O2));
-    oIz[i] = pk_max(pk_max(pk_sub(sZ, pa.E2), pk_sub(A3, pa.OE)), pk_sub(B3, pa.O2));
-    oIxy[i] = pk_max(pk_sub(C1, pa.E), pk_sub(D1, pa.O));
-    oIyz[i] = pk_max(pk_sub(C2, pa.E), pk_sub(D2, pa.O));
-    oIxz[i] = pk_max(pk_sub(C3, pa.E), pk_sub(D3, pa.O));
+    // GO >= GE: the highest-penalty group of every target may be widened to
+    // all 7 states (see cell_messages_f16), so it is the MAX7 minus one penalty
+    const uint32_t best = pk_max(pk_max(A1, A2), sM);  // A1 | A2 = the six gap states
+    const uint32_t bO = pk_sub(best, pa.O), bO2 = pk_sub(best, pa.O2);
+    oBest[i] = best;
+    nIx[i] = pk_max(pk_max(pk_sub(sX, pa.E2), pk_sub(A1, pa.OE)), bO2);
+    oIy[i] = pk_max(pk_max(pk_sub(sY, pa.E2), pk_sub(A2, pa.OE)), bO2);
+    oIz[i] = pk_max(pk_max(pk_sub(sZ, pa.E2), pk_sub(A3, pa.OE)), bO2);
+    oIxy[i] = pk_max(pk_sub(C1, pa.E), bO);
+    oIyz[i] = pk_max(pk_sub(C2, pa.E), bO);
+    oIxz[i] = pk_max(pk_sub(C3, pa.E), bO);
   }
 }
 
@@ -437,22 +437,23 @@ __device__ __forceinline__ void cell_messages_f16(
     const h2 A1 = hmax3(pYZ, sXY, sXZ);  // Ix  <- {Iy,Iz,Ixy,Ixz} at GO+GE
     const h2 A2 = hmax3(pXZ, sXY, sYZ);  // Iy  <- {Ix,Iz,Ixy,Iyz}
     const h2 A3 = hmax3(pXY, sYZ, sXZ);  // Iz  <- {Ix,Iy,Iyz,Ixz}
-    const h2 B1 = hmax(sM, sYZ);         // Ix  <- {M,Iyz} at 2GO
-    const h2 B2 = hmax(sM, sXZ);
-    const h2 B3 = hmax(sM, sXY);
     const h2 C1 = hmax(pXY, sXY);        // Ixy <- {Ix,Iy,Ixy} at GE
     const h2 C2 = hmax(pYZ, sYZ);
     const h2 C3 = hmax(pXZ, sXZ);
-    const h2 D1 = hmax3(B1, sZ, sXZ);    // Ixy <- {M,Iz,Iyz,Ixz} at GO
-    const h2 D2 = hmax3(B2, sX, sXY);
-    const h2 D3 = hmax3(B3, sY, sYZ);
-    oBest[i] = U(hmax3(A1, B1, sX));     // MAX7 of the states
-    nIx[i] = U(hmax3(sX - E2, A1 - OE, B1 - O2));
-    oIy[i] = U(hmax3(sY - E2, A2 - OE, B2 - O2));
-    oIz[i] = U(hmax3(sZ - E2, A3 - OE, B3 - O2));
-    oIxy[i] = U(hmax(C1 - E, D1 - O));
-    oIyz[i] = U(hmax(C2 - E, D2 - O));
-    oIxz[i] = U(hmax(C3 - E, D3 - O));
+    // With GO >= GE (pencil_supported) each target's highest penalty group
+    // ({M,Iyz} at 2GO for Ix, {M,Iz,Iyz,Ixz} at GO for Ixy, ...) may take in
+    // every other state too: those already reach the target at a penalty no
+    // larger (2GE <= GO+GE <= 2GO, GE <= GO). So that group is MAX7 - penalty,
+    // shared by the three single and the three pair targets.
+    const h2 best = hmax3(A1, A2, sM);   // A1 | A2 = the six gap states
+    const h2 bO = best - O, bO2 = best - O2;
+    oBest[i] = U(best);
+    nIx[i] = U(hmax3(sX - E2, A1 - OE, bO2));
+    oIy[i] = U(hmax3(sY - E2, A2 - OE, bO2));
+    oIz[i] = U(hmax3(sZ - E2, A3 - OE, bO2));
+    oIxy[i] = U(hmax(C1 - E, bO));
+    oIyz[i] = U(hmax(C2 - E, bO));
+    oIxz[i] = U(hmax(C3 - E, bO));
   }
 }
 

@@ -79,13 +79,14 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False):
         sM = inM + s3; sX, sY, sZ = inIx, inIy, inIz
         sXY, sYZ, sXZ = inIxy + s2ab, inIyz + s2bc, inIxz + s2ac
         mx = np.maximum
+        # GO >= GE: each target's highest-penalty group widened to all 7 states
         best = mx.reduce([sM, sX, sY, sZ, sXY, sYZ, sXZ])
-        nIx = mx.reduce([sX - E2, mx.reduce([sY, sZ, sXY, sXZ]) - OE, mx(sM, sYZ) - O2])
-        oIy = mx.reduce([sY - E2, mx.reduce([sX, sZ, sXY, sYZ]) - OE, mx(sM, sXZ) - O2])
-        oIz = mx.reduce([sZ - E2, mx.reduce([sX, sY, sYZ, sXZ]) - OE, mx(sM, sXY) - O2])
-        oIxy = mx(mx.reduce([sX, sY, sXY]) - E, mx.reduce([sM, sZ, sYZ, sXZ]) - O)
-        oIyz = mx(mx.reduce([sY, sZ, sYZ]) - E, mx.reduce([sM, sX, sXY, sXZ]) - O)
-        oIxz = mx(mx.reduce([sX, sZ, sXZ]) - E, mx.reduce([sM, sY, sXY, sYZ]) - O)
+        nIx = mx.reduce([sX - E2, mx.reduce([sY, sZ, sXY, sXZ]) - OE, best - O2])
+        oIy = mx.reduce([sY - E2, mx.reduce([sX, sZ, sXY, sYZ]) - OE, best - O2])
+        oIz = mx.reduce([sZ - E2, mx.reduce([sX, sY, sYZ, sXZ]) - OE, best - O2])
+        oIxy = mx(mx.reduce([sX, sY, sXY]) - E, best - O)
+        oIyz = mx(mx.reduce([sY, sZ, sYZ]) - E, best - O)
+        oIxz = mx(mx.reduce([sX, sZ, sXZ]) - E, best - O)
         recout = np.stack([oIy, oIxy, oIyz, best], -1)
         xr[:, t & 1] = recout
         last = recout[NW - 1].copy()
