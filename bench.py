@@ -165,6 +165,10 @@ def main():
         kind = "pencil" if _pencil_ok(tsa, L, params) else "plane"
     kernel_name = {"plane": "plane_step_kernel", "pencil": "pencil_kernel"}[kind]
     launches_per_step = (3 * L - 1) if kind == "plane" else 1
+    # kernel, arithmetic and schedule the library picks (host-only query)
+    plan = tsa.describe_plan(per_gpu, L, L, L, params, kernel=kind, sync=False)
+    # exact integer values in f16 / int16 lanes; plane: int32 math on int16 planes
+    arith = "f16" if " f16 " in plan else ("i32" if plan == "plane" else "i16")
 
     # per-rank kernel time of THIS rank's stream (HIP events on the launch stream)
     per_gpu_cells = n * cells_per_triple
@@ -269,13 +273,13 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "i16",
+        "dtype": arith,
         "data": "synthetic (splitmix64 uniform DNA, SURVEY.md 8d seeds)",
         "config": {
             "workload": (f"batch: {per_gpu} independent {L}^3 triples per GPU (configs[4] per-GPU shard)"
                          if args.workload == "batch" else f"single: one {L}^3 triple per GPU (configs[2])"),
             "length": L, "triples_per_gpu": per_gpu, "triples_total": n_total,
-            "kernel": kind, "launches_per_step": launches_per_step,
+            "kernel": kind, "plan": plan, "launches_per_step": launches_per_step,
             "parallelism": f"shard{world}", "score_bits": params.score_bits,
         },
         "roofline": {

@@ -59,7 +59,7 @@ SYMBOLS = {"A": 0, "T": 1, "C": 2, "G": 3, "N": 4}
 EXPORTS = (
     "tsa_default_params", "tsa_validate", "tsa_score_gpu", "tsa_score_gpu_ex",
     "tsa_score_batch", "tsa_batch_workspace_size", "tsa_score_batch_async",
-    "tsa_device_count", "tsa_strerror", "tsa_version",
+    "tsa_device_count", "tsa_strerror", "tsa_version", "tsa_describe_plan",
 )
 
 
@@ -119,13 +119,16 @@ def _load_lib() -> ctypes.CDLL:
                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, pp,
                                           ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_size_t, ctypes.c_void_p]
+    lib.tsa_describe_plan.argtypes = [ctypes.c_int32] * 4 + [pp, ctypes.c_int32, ctypes.c_int32,
+                                                            ctypes.c_char_p, ctypes.c_size_t]
     lib.tsa_device_count.argtypes = []
     lib.tsa_strerror.argtypes = [ctypes.c_int]
     lib.tsa_strerror.restype = ctypes.c_char_p
     lib.tsa_version.argtypes = []
     lib.tsa_version.restype = ctypes.c_char_p
     for name in ("tsa_validate", "tsa_score_gpu", "tsa_score_gpu_ex", "tsa_score_batch",
-                 "tsa_batch_workspace_size", "tsa_score_batch_async", "tsa_device_count"):
+                 "tsa_batch_workspace_size", "tsa_score_batch_async", "tsa_device_count",
+                 "tsa_describe_plan"):
         getattr(lib, name).restype = ctypes.c_int
     return lib
 
@@ -232,6 +235,19 @@ def workspace_size(n: int, max_la: int, max_lb: int, max_lc: int,
     _check(_lib.tsa_batch_workspace_size(n, max_la, max_lb, max_lc, ctypes.byref(p), k,
                                          ctypes.byref(sz)), "tsa_batch_workspace_size")
     return int(sz.value)
+
+
+def describe_plan(n: int, max_la: int, max_lb: int, max_lc: int,
+                  params: Optional[TsaParams] = None, kernel: str | int = "auto",
+                  sync: bool = True) -> str:
+    """The kernel, arithmetic and schedule a batch of these sizes runs
+    (tsa_describe_plan; host-only). ``sync``: the tsa_score_batch path."""
+    p = params or TsaParams.default()
+    k = KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
+    buf = ctypes.create_string_buffer(128)
+    _check(_lib.tsa_describe_plan(n, max_la, max_lb, max_lc, ctypes.byref(p), k, int(sync), buf,
+                                  len(buf)), "tsa_describe_plan")
+    return buf.value.decode()
 
 
 def score_batch_async(d_seqs_ptr: int, d_offsets_ptr: int, n: int, max_la: int, max_lb: int,

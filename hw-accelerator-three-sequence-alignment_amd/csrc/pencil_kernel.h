@@ -16,6 +16,9 @@ bool pencil_shape_supported(int32_t max_la, int32_t max_lb, int32_t max_lc);
 // rerun with stream_ok = false if it is set)
 size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
                               bool stream_ok);
+// The plan pencil_launch_batch would run, as text (tsa_describe_plan).
+void pencil_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
+                     const Range &bound, bool stream_ok, char *buf, size_t len);
 int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                         int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
                         const Range &bound, int32_t *d_scores, void *d_ws, size_t ws_bytes,

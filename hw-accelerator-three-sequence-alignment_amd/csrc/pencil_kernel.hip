@@ -1290,6 +1290,20 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
           : ((SOP_) ? LAUNCH<MM, NN, false, true>(__VA_ARGS__)                             \
                     : LAUNCH<MM, NN, false, false>(__VA_ARGS__)))
 
+void pencil_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
+                     const Range &bound, bool stream_ok, char *buf, size_t len) {
+  const char *arith = use_f16(kp, bound) ? "f16" : "i16";
+  const char *s3 = kp.s3_mode == TSA_S3_SOP ? "sop" : "rtl";
+  const LapGeom lg = lap_choice(n, max_la, max_lb, max_lc, stream_ok);
+  if (lg.ok) {
+    snprintf(buf, len, "pencil lap %s %s M=%d NW=%d laps=%d tiles=%d waves=%lld", arith, s3, lg.M,
+             lg.NW, lg.G, lg.GZ, (long long)lg.waves);
+    return;
+  }
+  const PencilGeom g = pencil_geom(max_la, max_lc);
+  snprintf(buf, len, "pencil helix %s %s M=%d NW=%d P=%d", arith, s3, g.M, helix_nw(g.M), g.P);
+}
+
 int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                         int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
                         const Range &bound, int32_t *d_scores, void *d_ws, size_t ws_bytes,

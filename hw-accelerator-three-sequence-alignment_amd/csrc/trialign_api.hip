@@ -343,6 +343,23 @@ int tsa_score_batch(const uint8_t *seqs, const int64_t *offsets, int32_t n, cons
   return TSA_OK;
 }
 
+int tsa_describe_plan(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
+                      const tsa_params *p, int32_t kernel, int32_t sync, char *buf, size_t len) {
+  if (!buf || len == 0 || n < 1 || max_la < 1 || max_lb < 1 || max_lc < 1 || !params_ok(p))
+    return TSA_EINVAL;
+  const int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
+  if (kind < 0) return TSA_ERANGE;
+  if (kind == TSA_KERNEL_PLANE) {
+    snprintf(buf, len, "plane");
+    return TSA_OK;
+  }
+  KParams kp;
+  build_kparams(p, &kp);
+  pencil_describe(std::min(n, 65535), max_la, max_lb, max_lc, kp,
+                  value_bound(p, max_la, max_lb, max_lc), sync != 0, buf, len);
+  return TSA_OK;
+}
+
 int tsa_batch_workspace_size(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
                              const tsa_params *p, int32_t kernel, size_t *bytes) {
   if (!bytes || n < 0 || max_la < 1 || max_lb < 1 || max_lc < 1 || !params_ok(p)) return TSA_EINVAL;

@@ -116,6 +116,15 @@ int tsa_score_batch_async(const uint8_t *d_seqs, const int64_t *d_offsets,
                           int32_t *d_scores, void *d_workspace,
                           size_t workspace_bytes, void *stream);
 
+/* Which kernel, arithmetic and schedule a batch of these sizes would run, as a
+ * short text such as "pencil lap f16 rtl M=1 NW=16 laps=16 tiles=1 waves=1"
+ * or "plane" (sync = 1: the synchronous tsa_score_batch path, which may stream
+ * the lap kernel). Host-only, no device needed. A diagnostic with no reference
+ * counterpart (the RTL has one fixed datapath). */
+int tsa_describe_plan(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
+                      const tsa_params *p, int32_t kernel, int32_t sync, char *buf,
+                      size_t len);
+
 /* Number of visible HIP devices (0 when none), or a negative code. */
 int tsa_device_count(void);
 

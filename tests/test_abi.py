@@ -79,6 +79,30 @@ def test_workspace_size(tsa):
         tsa.workspace_size(1, 0, 64, 64, p)
 
 
+def test_describe_plan(tsa):
+    # host-only plan query: the bench workload, the single-cube configs, the
+    # streaming lap window of the sync path, and parameter sets the pencil
+    # arithmetic does not cover
+    p = tsa.TsaParams.default()
+    assert tsa.describe_plan(512, 256, 256, 256, p).startswith("pencil helix f16 rtl M=2 NW=8")
+    assert tsa.describe_plan(1, 256, 256, 256, p).startswith("pencil lap f16 rtl M=1")
+    assert "waves=2" in tsa.describe_plan(32, 256, 256, 256, p, sync=True)
+    assert tsa.describe_plan(32, 256, 256, 256, p, sync=False).startswith("pencil helix")
+    p16 = tsa.TsaParams.default(score_bits=16)
+    assert tsa.describe_plan(1, 1024, 1024, 1024, p16).startswith("pencil lap i16 rtl")
+    sop = tsa.TsaParams.default(s3_mode=tsa.S3_SOP)
+    assert " sop " in tsa.describe_plan(512, 256, 256, 256, sop)
+    assert tsa.describe_plan(4, 64, 64, 64, p, kernel="plane") == "plane"
+    # gap_extend > gap_open: the widened message groups are not exact -> plane
+    ge = tsa.TsaParams.default(gap_open=1, gap_extend=2)
+    assert tsa.describe_plan(4, 64, 64, 64, ge) == "plane"
+    with pytest.raises(tsa.TsaError) as e:
+        tsa.describe_plan(4, 64, 64, 64, ge, kernel="pencil")
+    assert e.value.rc == tsa.TSA_ERANGE
+    # wrapping parameter sets stay on the literal plane kernel
+    assert tsa.describe_plan(4, 90, 90, 90, tsa.TsaParams.default(score_bits=6)) == "plane"
+
+
 @pytest.mark.skipif(os.environ.get("TSA_EXPECT_GPU") == "1", reason="GPU box")
 def test_no_cpu_fallback_without_gpu(tsa):
     if tsa.device_count() > 0:
