@@ -9,12 +9,14 @@
 //
 //  * one workgroup scores one triple; wave w of NW owns DP row y = lap*NW+w+1;
 //  * the 64 lanes x M packed int16 pairs own Zt = 128*M consecutive z
-//    positions k (lane l, pair i, half h -> k = l + 64h + 128i), z = k+1;
+//    positions k (lane l, register i, half h -> k = 64Mh + Ml + i), z = k+1:
+//    a lane's consecutive positions sit in consecutive registers;
 //  * position k of wave w computes cell x = u mod P + 1 of lap u div P at step
 //    t, with u = t - w - k (one step of skew per y and per z). A lane that
 //    finishes x = P of lap L continues with x = 1 of lap L+1 (row y+NW), so
 //    there is no fill/drain between rows: the positions form a helix;
-//  * z-1 neighbours arrive by one DPP wave_ror:1 + v_perm per packed value,
+//  * z-1 neighbours arrive by register renaming (i >= 1) and one DPP
+//    wave_ror:1 + v_perm for register 0, per message and step whatever M is,
 //    y-1 neighbours through a 2-slot LDS record per wave pair, and the wave
 //    above wave 0 (row y-1 of the previous lap) through a global ring that the
 //    last wave writes and wave 0 prefetches PD steps ahead with LDS-DMA;
@@ -67,6 +69,9 @@ __host__ __device__ constexpr int lap_pd(int M) {
 }
 constexpr int LAP_SLACK = TSA_LAP_SLACK;  // producer steps of row stores in flight
 constexpr int REC_BYTES = 16;      // {Iy, Ixy, Iyz, best} packed pairs per lane
+#ifndef TSA_A_PREFETCH  // read the next step's A codes before the step barrier
+#define TSA_A_PREFETCH 1
+#endif
 constexpr int RING_EXTRA = 8;
 
 // Packed (both halves) constants. int16 form: two's complement; exact-f16 form
@@ -457,21 +462,39 @@ __device__ __forceinline__ void cell_messages_f16(
   }
 }
 
-// Shift a packed per-position value one position up the helix (k <- k-1):
-// lanes >= 1 take lane-1's pair as is; lane 0 takes (pair i-1).hi and
-// (pair i).lo of lane 63; position 0 (lane 0, pair 0, lo) gets the z = 0 face.
-template <int M>
+// Shift a packed per-position value one position up the helix (k <- k-1).
+// With k = 64M*h + M*lane + i, register i >= 1 takes register i-1 of the same
+// lane (a rename, no instruction); register 0 takes register M-1 of lane-1
+// (one DPP wave_ror:1), except lane 0: its low half is position 0 and gets the
+// z = 0 face, its high half (position 64M) takes the low half of lane 63's
+// register M-1 -- one v_perm with a per-lane selector does both.
 // Only lane 0 reads the second v_perm source (its selector takes bytes 2..3 of
-// it), so for pair 0 that source is `face`, whose high half is the z = 0 face
-// (or, for a z-tile, the previous tile's last position) -- no extra v_bfi.
+// it), so that source is `face`, whose high half is the z = 0 face (or, for a
+// z-tile, the previous tile's last position) -- no extra v_bfi.
+template <int M>
 __device__ __forceinline__ void zshift(uint32_t (&v)[M], const uint32_t (&src)[M], uint32_t sel,
                                        uint32_t face) {
-  uint32_t r[M];
+  const uint32_t r = ror1(src[M - 1]);
 #pragma unroll
-  for (int i = 0; i < M; ++i) r[i] = ror1(src[i]);
-  v[0] = __builtin_amdgcn_perm(r[0], face, sel);
+  for (int i = M - 1; i >= 1; --i) v[i] = src[i - 1];
+  v[0] = __builtin_amdgcn_perm(r, face, sel);
+}
+// A codes of a lane's M registers: entries va, va-4, ... of the LDS table
+// (register i holds position M*lane+i, one x behind register i-1).
+template <int M>
+__device__ __forceinline__ void load_a(uint32_t va, uint32_t (&a)[M]) {
 #pragma unroll
-  for (int i = 1; i < M; ++i) v[i] = __builtin_amdgcn_perm(r[i], r[i - 1], sel);
+  for (int i = 0; i < M; ++i)
+    a[i] = *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t)(
+        va + 4u * (uint32_t)(M - 1 - i));
+}
+// Position k -> (lane, register, half) of the layout above.
+template <int M>
+__device__ __forceinline__ void pos_split(int32_t k, int32_t &l, int32_t &i, int32_t &h) {
+  h = k >= 64 * M;
+  const int32_t r = k - h * 64 * M;
+  l = r / M;
+  i = r % M;
 }
 
 // The step lambdas are left to the regular inliner for M <= 2 (an early forced
@@ -523,9 +546,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
   uint32_t fsv = pa.f_single, fpv = pa.f_pair;  // VGPR copies for v_bfi_b32 / v_pk_mad_u16
   uint32_t sbcv = pa.h_sbc, kdv = pa.h_kd, k0v = pa.h_k0, one1 = 0x00010001u;
   asm volatile("" : "+v"(fsv), "+v"(fpv), "+v"(sbcv), "+v"(kdv), "+v"(k0v), "+v"(one1));
-  // a[i] of this lane at step t is sA2[(t-w) mod P + ZT - lane - 128 i]
+  // a[i] of this lane at step t is sA2[(t-w) mod P + ZT - M lane - i]
   const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
-                          4u * (uint32_t)(ZT - lane - 128 * (M - 1));
+                          4u * (uint32_t)(ZT - M * lane - (M - 1));
 
   for (int tri = blockIdx.x; tri < n; tri += gridDim.x) {
     const int64_t o0 = offs[3 * (int64_t)tri], o1 = offs[3 * (int64_t)tri + 1];
@@ -533,9 +556,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     const int32_t la = (int32_t)(o1 - o0), lb = (int32_t)(o2 - o1), lc = (int32_t)(o3 - o2);
     uint8_t *ring = ring_base + (int64_t)blockIdx.x * ring_stride;
 
-    // ---- stage A codes (padded to P, pairs k/k+64) and B; face records in the ring
+    // ---- stage A codes (padded to P, halves k/k+64M) and B; face records in the ring
     for (int j = threadIdx.x; j < P + ZT; j += 64 * NW) {
-      const int x0 = ((j - ZT) % P + P) % P, x1 = ((j - ZT - 64) % P + P) % P;
+      const int x0 = ((j - ZT) % P + P) % P, x1 = ((j - ZT - 64 * M) % P + P) % P;
       const uint32_t c0 = x0 < la ? SYM0 << (seqs[o0 + x0] & 3) : 0u;
       const uint32_t c1 = x1 < la ? SYM0 << (seqs[o0 + x1] & 3) : 0u;
       sA2[j] = c0 | (c1 << 16);
@@ -555,7 +578,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     uint32_t oIx[M], shIz[M], svIxy[M], svIyz[M], shIxz[2][M], svM[2][M];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
-      const int k0 = lane + 128 * i, k1 = lane + 64 + 128 * i;
+      const int k0 = M * lane + i, k1 = 64 * M + M * lane + i;
       const uint32_t c0 = k0 < lc ? SYM0 << (seqs[o2 + k0] & 3) : 0u;
       const uint32_t c1 = k1 < lc ? SYM0 << (seqs[o2 + k1] & 3) : 0u;
       c[i] = c0 | (c1 << 16);
@@ -592,6 +615,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       }
     }
     int32_t dma_row = ((PD - lag) % R + R) % R;  // ring row for step t + PD
+    uint32_t a_nx[M];                            // A codes of the coming step
+    if constexpr (TSA_A_PREFETCH) load_a<M>(a_lane + 4u * (uint32_t)xpos0, a_nx);
     int32_t st_row = 0;                          // ring row written at step t (last wave)
 
     // One step; PH = t & 1 picks the register roles and the LDS record slots,
@@ -602,12 +627,11 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       constexpr int ROLE = decltype(role)::value;
       // this step's A codes (LDS table) and the B code of position x = 1
       uint32_t a[M];
-      {
-        const uint32_t va = a_lane + 4u * (uint32_t)xpos0;
+      if constexpr (TSA_A_PREFETCH) {
 #pragma unroll
-        for (int i = 0; i < M; ++i)
-          a[i] = *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t)(
-              va + 512u * (uint32_t)(M - 1 - i));
+        for (int i = 0; i < M; ++i) a[i] = a_nx[i];
+      } else {
+        load_a<M>(a_lane + 4u * (uint32_t)xpos0, a);
       }
       // ---- receive the wave-above record of step t-1
       uint4 rec[M];
@@ -636,9 +660,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       // face (EN_i==1&&EN==0 gating, src/PE_1cyc.v:164-178,196-202,212-218), and
       // it starts row lap0*NW+w+1, whose B symbol it takes here.
       if (xpos0 < ZT) {
-        const uint32_t hm = (xpos0 >> 6) & 1 ? 0xFFFF0000u : 0x0000FFFFu;
-        const uint32_t m1 = lane == (xpos0 & 63) ? hm : 0u;
-        const int is = xpos0 >> 7;
+        int32_t ls, is, hs;
+        pos_split<M>(xpos0, ls, is, hs);
+        const uint32_t hm = hs ? 0xFFFF0000u : 0x0000FFFFu;
+        const uint32_t m1 = lane == ls ? hm : 0u;
 #pragma unroll
         for (int i = 0; i < M; ++i) {
           if (i == is) {
@@ -692,8 +717,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
           const int32_t lim = t - w;  // position k started iff k <= lim
 #pragma unroll
           for (int i = 0; i < M; ++i) {
-            const uint32_t m = ((lane + 128 * i > lim) ? 0x0000FFFFu : 0u) |
-                               ((lane + 64 + 128 * i > lim) ? 0xFFFF0000u : 0u);
+            const uint32_t m = ((M * lane + i > lim) ? 0x0000FFFFu : 0u) |
+                               ((64 * M + M * lane + i > lim) ? 0xFFFF0000u : 0u);
             oIy[i] = bfi(m, pa.f_single, oIy[i]);
             oIxy[i] = bfi(m, pa.f_pair, oIxy[i]);
             oIyz[i] = bfi(m, pa.f_pair, oIyz[i]);
@@ -723,6 +748,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         xpos0 = 0;
         binj = b_of_lap(++lap0);
       }
+      if constexpr (TSA_A_PREFETCH) load_a<M>(a_lane + 4u * (uint32_t)xpos0, a_nx);
 
       // ---- wave 0: fetch the record of step t + PD into the slot just consumed
       if constexpr (ROLE == 0) {
@@ -754,7 +780,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      const int32_t l_f = k_f & 63, i_f = k_f >> 7, h_f = (k_f >> 6) & 1;
+      int32_t l_f, i_f, h_f;
+      pos_split<M>(k_f, l_f, i_f, h_f);
       const uint32_t v = fin[i_f * 64 + l_f];
       const uint16_t hb = (uint16_t)(h_f ? (v >> 16) : (v & 0xFFFF));
       scores[tri] = F16 ? (int32_t)(float)__builtin_bit_cast(_Float16, hb) : (int32_t)(int16_t)hb;
@@ -860,17 +887,17 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
   int32_t *flag_mine = flags + wg;
   const int32_t *flag_prev = flag_mine - GZ, *flag_zprev = flag_mine - 1;
 
-  // A code pairs: entry j holds x = j-ZT (lo) and x = j-ZT-64 (hi), 0 outside [0, la)
+  // A code pairs: entry j holds x = j-ZT (lo) and x = j-ZT-64M (hi), 0 outside [0, la)
   const int32_t na = lds_a / 4;
   for (int j = threadIdx.x; j < na; j += 64 * NW) {
-    const int x0 = j - ZT, x1 = j - ZT - 64;
+    const int x0 = j - ZT, x1 = j - ZT - 64 * M;
     const uint32_t c0 = (x0 >= 0 && x0 < la) ? SYM0 << (seqs[o0 + x0] & 3) : 0u;
     const uint32_t c1 = (x1 >= 0 && x1 < la) ? SYM0 << (seqs[o0 + x1] & 3) : 0u;
     sA2[j] = c0 | (c1 << 16);
   }
-  // position k of this wave is at x-1 = t - w - k: a[i] = sA2[t - w + ZT - lane - 128 i]
+  // position k of this wave is at x-1 = t - w - k: a[i] = sA2[t - w + ZT - M lane - i]
   const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
-                          4u * (uint32_t)(ZT - w - lane - 128 * (M - 1));
+                          4u * (uint32_t)(ZT - w - M * lane - (M - 1));
 
   const int32_t y = L * NW + w + 1;  // this wave's DP row
   const uint32_t bw = y <= lb ? (SYM0 << (seqs[o1 + y - 1] & 3)) * 0x00010001u : 0u;
@@ -882,7 +909,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     const int64_t oc = o2 + (int64_t)q * ZT;
 #pragma unroll
     for (int i = 0; i < M; ++i) {
-      const int k0 = lane + 128 * i, k1 = lane + 64 + 128 * i;
+      const int k0 = M * lane + i, k1 = 64 * M + M * lane + i;
       const uint32_t c0 = k0 < zt_q ? SYM0 << (seqs[oc + k0] & 3) : 0u;
       const uint32_t c1 = k1 < zt_q ? SYM0 << (seqs[oc + k1] & 3) : 0u;
       c[i] = c0 | (c1 << 16);
@@ -951,6 +978,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
   __syncthreads();
   stamp(1);
   const uint4 face = make_uint4(pa.f_single, pa.f_pair, pa.f_pair, 0u);
+  uint32_t a_nx[M];  // A codes of the coming step
+  if constexpr (TSA_A_PREFETCH) load_a<M>(a_lane, a_nx);
 
   // ROLE (wave 0): bit 0 = rows of lap L-1 arrive (L > 0), bit 2 = z records of
   // tile q-1 arrive (q > 0); 2 = middle waves; 3 = the last wave
@@ -960,12 +989,12 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     constexpr bool W0 = ROLE == 0 || ROLE == 1 || ROLE == 4 || ROLE == 5;
     constexpr bool YIN = ROLE == 1 || ROLE == 5, ZIN0 = ROLE == 4 || ROLE == 5;
     uint32_t a[M];
-    {
-      const uint32_t va = a_lane + 4u * (uint32_t)t;
+    if constexpr (TSA_A_PREFETCH) {
 #pragma unroll
-      for (int i = 0; i < M; ++i)
-        a[i] = *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t)(
-            va + 512u * (uint32_t)(M - 1 - i));
+      for (int i = 0; i < M; ++i) a[i] = a_nx[i];
+      load_a<M>(a_lane + 4u * (uint32_t)(t + 1), a_nx);  // lands by the step barrier
+    } else {
+      load_a<M>(a_lane + 4u * (uint32_t)t, a);
     }
     uint4 rec[M];
     if constexpr (W0) {
@@ -1007,9 +1036,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     // x == 1 at position k* = t - w: x = 0 face inputs (src/PE_1cyc.v:164-178,196-218)
     const int32_t ks = t - w;
     if (ks >= 0 && ks < ZT) {
-      const uint32_t hm = (ks >> 6) & 1 ? 0xFFFF0000u : 0x0000FFFFu;
-      const uint32_t m1 = lane == (ks & 63) ? hm : 0u;
-      const int is = ks >> 7;
+      int32_t ls, is, hs;
+      pos_split<M>(ks, ls, is, hs);
+      const uint32_t hm = hs ? 0xFFFF0000u : 0x0000FFFFu;
+      const uint32_t m1 = lane == ls ? hm : 0u;
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         if (i == is) {
@@ -1142,7 +1172,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (final_wg) {
     if (threadIdx.x == 0) {
-      const int32_t l_f = k_f & 63, i_f = k_f >> 7, h_f = (k_f >> 6) & 1;
+      int32_t l_f, i_f, h_f;
+      pos_split<M>(k_f, l_f, i_f, h_f);
       const uint32_t v = fin[i_f * 64 + l_f];
       const uint16_t hb = (uint16_t)(h_f ? (v >> 16) : (v & 0xFFFF));
       scores[tri] = F16 ? (int32_t)(float)__builtin_bit_cast(_Float16, hb) : (int32_t)(int16_t)hb;

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Build a variant of the package into scratch/<name>/ (same sources, extra -D
+# flags) for same-box A/B timing: TSA_PKG_DIR=scratch/<name> selects it.
+#   scripts/build_variant.sh nopf "-DTSA_A_PREFETCH=0"
+set -e
+cd "$(dirname "$0")/.."
+NAME=$1; DEFS=$2
+PKG=hw-accelerator-three-sequence-alignment_amd
+OUT=scratch/$NAME
+rm -rf "$OUT"; mkdir -p "$OUT/lib" "$OUT/build"
+cp $PKG/*.py "$OUT/"
+objs=()
+for f in $PKG/csrc/*.hip; do
+  o="$OUT/build/$(basename "${f%.hip}").o"
+  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function \
+    -DTSA_GIT_DESCRIBE="\"variant-$NAME\"" $DEFS -c "$f" -o "$o" &
+  objs+=("$o")
+done
+wait
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -shared -o "$OUT/lib/libtrialign.so" "${objs[@]}" -lpthread
+rm -rf "$OUT/build"
+echo "built $OUT"

@@ -9,7 +9,7 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_
            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SALU SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace -d "$OUT/p$i" -o run --output-format csv \
-    -- python3 "$R/tools/bench_variants.py" --n ${N:-512} --rounds 1 --variants ${VARIANTS:-TSA_PENCIL_NW=16} \
+    -- python3 "$R/tools/bench_variants.py" --n ${N:-512} --rounds 3 --variants ${VARIANTS:-TSA_PENCIL_NW=8} \
     > "$OUT/p$i.json" 2> "$OUT/p$i.err"
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$OUT/p$i.err"; exit $rc; }
 done

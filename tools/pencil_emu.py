@@ -1,7 +1,7 @@
 """CPU emulation of the pencil kernel's schedule (pencil_kernel.hip) -- a
 debugging aid. Arrays are [wave][lane][pair][half] int32; every step mirrors
 the kernel's receive / substitute / compute / send / shift sequence, with the
-same helix position mapping k = lane + 64*half + 128*pair."""
+same helix position mapping k = 64*M*half + M*lane + pair."""
 import sys
 import numpy as np
 
@@ -21,7 +21,7 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False):
     sA = np.array([oh(a[i]) if i < la else 0 for i in range(P)])
     sB = np.array([oh(b[i]) if i < lb else 0 for i in range(4096)])
     lane = np.arange(64)
-    k = lane[:, None, None] + 64 * np.arange(2)[None, None, :] + 128 * np.arange(M)[None, :, None]  # [64][M][2]
+    k = M * lane[:, None, None] + 64 * M * np.arange(2)[None, None, :] + np.arange(M)[None, :, None]  # [64][M][2]
     cpos = np.where(k < lc, np.array([oh(c[j]) if j < lc else 0 for j in range(ZT)])[np.minimum(k, ZT - 1)], 0)
     W = np.arange(NW)[:, None, None, None]
     shape = (NW, 64, M, 2)
@@ -41,18 +41,16 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False):
     lap0 = np.array([0 if w == 0 else -1 for w in range(NW)])
     lap_f, w_f, k_f = (lb - 1) // NW, (lb - 1) % NW, lc - 1
     t_f = lap_f * P + (la - 1) + w_f + k_f
-    l_f, i_f, h_f = k_f & 63, k_f >> 7, (k_f >> 6) & 1
+    h_f = k_f // (64 * M); l_f, i_f = divmod(k_f - 64 * M * h_f, M)
+    order = np.argsort(k.reshape(-1))  # flat (lane, pair, half) index of position 0, 1, ...
 
     def shift(v, inj):
         # position k <- k-1 along the helix; position 0 gets inj (per wave)
-        out = np.empty_like(v)
-        out[:, 1:] = v[:, :-1]
-        # lane 0: lo <- lane63 pair i-1 hi ; hi <- lane63 pair i lo
-        for i in range(M):
-            out[:, 0, i, 0] = v[:, 63, (i - 1) % M, 1]
-            out[:, 0, i, 1] = v[:, 63, i, 0]
-        out[:, 0, 0, 0] = inj
-        return out
+        flat = v.reshape(v.shape[0], -1)
+        out = np.empty_like(flat)
+        out[:, order[1:]] = flat[:, order[:-1]]
+        out[:, order[0]] = inj
+        return out.reshape(v.shape)
 
     score = None
     for t in range(t_f + 1):
@@ -64,7 +62,7 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False):
         for w in range(NW):
             ks = xpos0[w]
             if ks < ZT:
-                l, h, i = ks & 63, (ks >> 6) & 1, ks >> 7
+                h = ks // (64 * M); l, i = divmod(ks - 64 * M * h, M)
                 inIx[w, l, i, h] = f_single; inIxy[w, l, i, h] = f_pair
                 inIxz[w, l, i, h] = f_pair; inM[w, l, i, h] = 0
         eab = (areg & breg) != 0
