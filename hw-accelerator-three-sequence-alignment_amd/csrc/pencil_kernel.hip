@@ -72,6 +72,22 @@ constexpr int REC_BYTES = 16;      // {Iy, Ixy, Iyz, best} packed pairs per lane
 #ifndef TSA_A_PREFETCH  // read the next step's A codes before the step barrier
 #define TSA_A_PREFETCH 1
 #endif
+// A/B knobs of the f16 cell (build-time; see scripts/build_variant.sh)
+#ifndef TSA_DMC        // a&c match term through a per-position scaled delta (no min)
+#define TSA_DMC 1
+#endif
+#ifndef TSA_VMAX3_ASM  // message maxes as explicit v_pk_maximum3_f16 (measured slower:
+#define TSA_VMAX3_ASM 0   // the asm blocks constrain the scheduler more than they save)
+#endif
+#ifndef TSA_GROUPS     // widened GO+GE groups sharing max(Ix,Iy,Iz)
+#define TSA_GROUPS 1
+#endif
+#ifndef TSA_LANE_MASK  // x = 1 lane mask from a scalar shift (one v_cndmask)
+#define TSA_LANE_MASK 1
+#endif
+#ifndef TSA_ROW_NEXT   // next row's per-row terms precomputed once per lap
+#define TSA_ROW_NEXT 1
+#endif
 constexpr int RING_EXTRA = 8;
 
 // Packed (both halves) constants. int16 form: two's complement; exact-f16 form
@@ -84,6 +100,7 @@ struct PencilArgs {
   uint32_t s3_d1, s3_d0, s3_ne; // RTL: s3 = ne + eab*(d0 + ebc*d1)
   uint32_t h_dm, h_c3;           // 2^13 (match-mismatch); RTL ne
   uint32_t h_sbc, h_k0, h_kd;     // per-row registers, see cell_messages_f16
+  float dmf;                      // match - mismatch (per-position DMC, exact f16)
   int32_t sop;                  // TSA_S3_SOP
 };
 
@@ -361,6 +378,7 @@ __device__ __forceinline__ void cell_messages(
     const uint32_t sXY = pk_add(inIxy[i], s2ab);
     const uint32_t sYZ = pk_add(inIyz[i], s2bc);
     const uint32_t sXZ = pk_add(inIxz[i], s2ac);
+    // two-input maxes only (no packed int16 max3): pairs shared between groups
     const uint32_t pYZ = pk_max(sY, sZ), pXZ = pk_max(sX, sZ), pXY = pk_max(sX, sY);
     const uint32_t qXY_XZ = pk_max(sXY, sXZ), qXY_YZ = pk_max(sXY, sYZ), qYZ_XZ = pk_max(sYZ, sXZ);
     const uint32_t A1 = pk_max(pYZ, qXY_XZ);  // Ix  <- {Iy,Iz,Ixy,Ixz} at GO+GE
@@ -407,12 +425,37 @@ __device__ __forceinline__ h2 H(uint32_t v) { return __builtin_bit_cast(h2, v); 
 __device__ __forceinline__ uint32_t U(h2 v) { return __builtin_bit_cast(uint32_t, v); }
 __device__ __forceinline__ h2 hmax(h2 a, h2 b) { return __builtin_elementwise_maximum(a, b); }
 __device__ __forceinline__ h2 hmax3(h2 a, h2 b, h2 c) { return hmax(hmax(a, b), c); }
+// One v_pk_maximum3_f16 exactly: left to itself the compiler CSEs the shared
+// two-input maxes of the message groups and then cannot fuse them into max3s.
+__device__ __forceinline__ h2 vmax3(h2 a, h2 b, h2 c) {
+#if TSA_VMAX3_ASM
+  h2 r;
+  asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+#else
+  return hmax3(a, b, c);
+#endif
+}
 __device__ __forceinline__ h2 hfma(h2 a, h2 b, h2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ uint32_t umin2(uint32_t a, uint32_t b) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(us2, a),
                                                                  __builtin_bit_cast(us2, b)));
 }
 constexpr uint32_t SYM0 = 0x800u;  // helix symbol codes: SYM0 << s
+// Per half: f16(dm / f16value(code)) for a one-hot code (a power of two:
+// 2^-13, 2^-11, 2^-7 or 2), 0 for code 0 (padding); exact for |dm| <= 7.
+__device__ __forceinline__ uint32_t dm_over_code(float dm, uint32_t codes) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint16_t c = (uint16_t)(codes >> (16 * h));
+    if (c != 0) {
+      const _Float16 v = (_Float16)(dm / (float)__builtin_bit_cast(_Float16, c));
+      r |= (uint32_t)__builtin_bit_cast(uint16_t, v) << (16 * h);
+    }
+  }
+  return r;
+}
 
 // Terms that depend only on (b, c) are per-position constants for a whole row
 // (b changes when a position starts a new row at x = 1), kept in registers:
@@ -422,7 +465,8 @@ constexpr uint32_t SYM0 = 0x800u;  // helix symbol codes: SYM0 << s
 template <int M, bool SOP>
 __device__ __forceinline__ void cell_messages_f16(
     const uint32_t (&a)[M], const uint32_t (&b)[M], const uint32_t (&c)[M],
-    const uint32_t (&SBC)[M], const uint32_t (&K)[M], uint32_t Q, const PencilArgs &pa,
+    const uint32_t (&SBC)[M], const uint32_t (&K)[M], const uint32_t (&DMC)[M], uint32_t Q,
+    const PencilArgs &pa,
     const uint32_t (&inIx)[M], const uint32_t (&inIy)[M], const uint32_t (&inIz)[M],
     const uint32_t (&inIxy)[M], const uint32_t (&inIyz)[M], const uint32_t (&inIxz)[M],
     const uint32_t (&inM)[M], uint32_t (&nIx)[M], uint32_t (&oIy)[M], uint32_t (&oIz)[M],
@@ -430,35 +474,53 @@ __device__ __forceinline__ void cell_messages_f16(
   const h2 DM = H(pa.h_dm), E = H(pa.E), O = H(pa.O), E2 = H(pa.E2), OE = H(pa.OE), O2 = H(pa.O2);
 #pragma unroll
   for (int i = 0; i < M; ++i) {
+    // a & c is c's code (a power of two) on a match, 0 otherwise, and
+    // DMC = (match - mismatch) / code(c) per position: the product is exact
+#if TSA_DMC
+    const h2 eab = H(umin2(a[i] & b[i], Q)), eac = H(a[i] & c[i]);
+    const h2 DMCi = H(DMC[i]);
+#else
     const h2 eab = H(umin2(a[i] & b[i], Q)), eac = H(umin2(a[i] & c[i], Q));
+    const h2 DMCi = DM;
+#endif
     const h2 sXY = hfma(eab, DM, H(inIxy[i]));  // src/PE_1cyc.v:159-161 (+mismatch folded)
-    const h2 sXZ = hfma(eac, DM, H(inIxz[i]));
+    const h2 sXZ = hfma(eac, DMCi, H(inIxz[i]));
     const h2 sYZ = H(inIyz[i]) + H(SBC[i]);
     h2 sM;                                       // src/PE_1cyc.v:162
-    if constexpr (SOP) sM = hfma(eab, DM, hfma(eac, DM, H(inM[i]))) + H(K[i]);
+    if constexpr (SOP) sM = hfma(eab, DM, hfma(eac, DMCi, H(inM[i]))) + H(K[i]);
     else sM = hfma(eab, H(K[i]), H(inM[i])) + H(pa.h_c3);  // ne + [a=b](d0 + [b=c] d1)
     const h2 sX = H(inIx[i]), sY = H(inIy[i]), sZ = H(inIz[i]);
+    // With GO >= GE (pencil_supported) a penalty group may take in any state
+    // that already reaches the target at a penalty no larger (2GE <= GO+GE <=
+    // 2GO, GE <= GO): each single target's GO+GE group takes in the target's
+    // own state, so the three share max(Ix,Iy,Iz); each target's highest
+    // group ({M,Iyz} at 2GO for Ix, {M,Iz,Iyz,Ixz} at GO for Ixy, ...) takes in
+    // all 7, so it is MAX7 - penalty, shared by all six gap targets.
+#if TSA_GROUPS
+    // vmax3(a, b, c) = max(max(a, b), c): the inner pairs are all distinct, so
+    // the compiler cannot CSE one and fuses every pair into one max3
+    const h2 S3 = vmax3(sX, sY, sZ);
+    const h2 A1 = vmax3(S3, sXY, sXZ);   // Ix  <- {Iy,Iz,Ixy,Ixz} (+Ix) at GO+GE
+    const h2 A2 = vmax3(S3, sYZ, sXY);   // Iy  <- {Ix,Iz,Ixy,Iyz} (+Iy)
+    const h2 A3 = vmax3(sYZ, sXZ, S3);   // Iz  <- {Ix,Iy,Iyz,Ixz} (+Iz)
+    const h2 C1 = vmax3(sX, sXY, sY);    // Ixy <- {Ix,Iy,Ixy} at GE
+    const h2 C2 = vmax3(sY, sYZ, sZ);
+    const h2 C3 = vmax3(sZ, sXZ, sX);
+    const h2 best = vmax3(A1, sYZ, sM);  // A1 | Iyz = the six gap states
+#else
     const h2 pYZ = hmax(sY, sZ), pXZ = hmax(sX, sZ), pXY = hmax(sX, sY);
-    const h2 A1 = hmax3(pYZ, sXY, sXZ);  // Ix  <- {Iy,Iz,Ixy,Ixz} at GO+GE
-    const h2 A2 = hmax3(pXZ, sXY, sYZ);  // Iy  <- {Ix,Iz,Ixy,Iyz}
-    const h2 A3 = hmax3(pXY, sYZ, sXZ);  // Iz  <- {Ix,Iy,Iyz,Ixz}
-    const h2 C1 = hmax(pXY, sXY);        // Ixy <- {Ix,Iy,Ixy} at GE
-    const h2 C2 = hmax(pYZ, sYZ);
-    const h2 C3 = hmax(pXZ, sXZ);
-    // With GO >= GE (pencil_supported) each target's highest penalty group
-    // ({M,Iyz} at 2GO for Ix, {M,Iz,Iyz,Ixz} at GO for Ixy, ...) may take in
-    // every other state too: those already reach the target at a penalty no
-    // larger (2GE <= GO+GE <= 2GO, GE <= GO). So that group is MAX7 - penalty,
-    // shared by the three single and the three pair targets.
-    const h2 best = hmax3(A1, A2, sM);   // A1 | A2 = the six gap states
+    const h2 A1 = hmax3(pYZ, sXY, sXZ), A2 = hmax3(pXZ, sXY, sYZ), A3 = hmax3(pXY, sYZ, sXZ);
+    const h2 C1 = hmax(pXY, sXY), C2 = hmax(pYZ, sYZ), C3 = hmax(pXZ, sXZ);
+    const h2 best = hmax3(A1, A2, sM);
+#endif
     const h2 bO = best - O, bO2 = best - O2;
     oBest[i] = U(best);
-    nIx[i] = U(hmax3(sX - E2, A1 - OE, bO2));
-    oIy[i] = U(hmax3(sY - E2, A2 - OE, bO2));
-    oIz[i] = U(hmax3(sZ - E2, A3 - OE, bO2));
-    oIxy[i] = U(hmax(C1 - E, bO));
-    oIyz[i] = U(hmax(C2 - E, bO));
-    oIxz[i] = U(hmax(C3 - E, bO));
+    nIx[i] = U(vmax3(sX - E2, A1 - OE, bO2));
+    oIy[i] = U(vmax3(sY - E2, A2 - OE, bO2));
+    oIz[i] = U(vmax3(sZ - E2, A3 - OE, bO2));
+    oIxy[i] = U(vmax3(C1 - E, bO, bO));
+    oIyz[i] = U(vmax3(C2 - E, bO, bO));
+    oIxz[i] = U(vmax3(C3 - E, bO, bO));
   }
 }
 
@@ -487,6 +549,18 @@ __device__ __forceinline__ void load_a(uint32_t va, uint32_t (&a)[M]) {
   for (int i = 0; i < M; ++i)
     a[i] = *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t)(
         va + 4u * (uint32_t)(M - 1 - i));
+}
+// bfi mask selecting one half (hs) of one lane (ls): the lane bit comes from a
+// scalar shift, so this is one VALU op (v_cndmask with an SGPR-pair mask);
+// the two asm strings differ so the compiler does not merge them into one
+// with a VALU-selected operand.
+__device__ __forceinline__ uint32_t lane_half_mask(int32_t ls, int32_t hs, uint32_t hmLo,
+                                                   uint32_t hmHi) {
+  const uint64_t lm = 1ull << ls;
+  uint32_t m;
+  if (hs) asm("v_cndmask_b32_e64 %0, 0, %1, %2 ; hi" : "=v"(m) : "v"(hmHi), "s"(lm));
+  else asm("v_cndmask_b32_e64 %0, 0, %1, %2 ; lo" : "=v"(m) : "v"(hmLo), "s"(lm));
+  return m;
 }
 // Position k -> (lane, register, half) of the layout above.
 template <int M>
@@ -545,7 +619,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
   const PencilArgs pv = F16 ? pa : pin_score_consts(pa);
   uint32_t fsv = pa.f_single, fpv = pa.f_pair;  // VGPR copies for v_bfi_b32 / v_pk_mad_u16
   uint32_t sbcv = pa.h_sbc, kdv = pa.h_kd, k0v = pa.h_k0, one1 = 0x00010001u;
+  uint32_t hmLo = 0x0000FFFFu, hmHi = 0xFFFF0000u, zero = 0u;
   asm volatile("" : "+v"(fsv), "+v"(fpv), "+v"(sbcv), "+v"(kdv), "+v"(k0v), "+v"(one1));
+  asm volatile("" : "+v"(hmLo), "+v"(hmHi), "+v"(zero));
   // a[i] of this lane at step t is sA2[(t-w) mod P + ZT - M lane - i]
   const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
                           4u * (uint32_t)(ZT - M * lane - (M - 1));
@@ -574,7 +650,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     __syncthreads();
 
     // ---- per-position registers (arrays [2] alternate roles between even/odd steps)
-    uint32_t b[M], c[M], SBC[M], K[M];
+    uint32_t b[M], c[M], SBC[M], K[M], DMC[M];
     uint32_t oIx[M], shIz[M], svIxy[M], svIyz[M], shIxz[2][M], svM[2][M];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
@@ -582,6 +658,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       const uint32_t c0 = k0 < lc ? SYM0 << (seqs[o2 + k0] & 3) : 0u;
       const uint32_t c1 = k1 < lc ? SYM0 << (seqs[o2 + k1] & 3) : 0u;
       c[i] = c0 | (c1 << 16);
+      DMC[i] = dm_over_code(pa.dmf, c[i]);
       b[i] = SBC[i] = K[i] = 0;  // set when a position reaches x = 1 of its lap
       oIx[i] = pa.f_single;
       shIz[i] = pa.f_single;
@@ -598,6 +675,20 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       return (lp >= 0 && r < lb) ? sB[r] : 0u;
     };
     uint32_t binj = b_of_lap(lap0);
+    // the per-row terms of the row whose B code is binj, for every position:
+    // a position copies them when it reaches x = 1 (recomputed once per lap)
+    uint32_t SBCn[M], Kn[M];
+    auto row_terms = [&]() {
+      if constexpr (F16 && TSA_ROW_NEXT) {
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          const uint32_t e01 = pk_eq1(binj, c[i], one1);
+          SBCn[i] = pk_mad(e01, sbcv, 0u);
+          Kn[i] = pk_mad(e01, kdv, k0v);
+        }
+      }
+    };
+    row_terms();
     const int32_t lap_f = (lb - 1) / NW, w_f = (lb - 1) % NW, k_f = lc - 1;
     const int32_t t_f = lap_f * P + (la - 1) + w_f + k_f;  // final cell (la, lb, lc)
     const int32_t T = t_f + 1;
@@ -662,33 +753,44 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       if (xpos0 < ZT) {
         int32_t ls, is, hs;
         pos_split<M>(xpos0, ls, is, hs);
-        const uint32_t hm = hs ? 0xFFFF0000u : 0x0000FFFFu;
-        const uint32_t m1 = lane == ls ? hm : 0u;
+#if TSA_LANE_MASK
+        const uint32_t m1 = lane_half_mask(ls, hs, hmLo, hmHi);
+#else
+        const uint32_t m1 = lane == ls ? (hs ? 0xFFFF0000u : 0x0000FFFFu) : 0u;
+#endif
 #pragma unroll
         for (int i = 0; i < M; ++i) {
           if (i == is) {
             inIx[i] = vbfi(m1, fsv, inIx[i]);
             inIxy[i] = vbfi(m1, fpv, inIxy[i]);
             inIxz[i] = vbfi(m1, fpv, inIxz[i]);
-            inM[i] = vbfi(m1, 0u, inM[i]);
+            inM[i] = vbfi(m1, zero, inM[i]);
             b[i] = vbfi(m1, binj, b[i]);
-            if constexpr (F16) {  // re-derive the pair's per-row terms from the new b
+            if constexpr (F16) {  // the new row's per-row terms
+#if TSA_ROW_NEXT
+              SBC[i] = vbfi(m1, SBCn[i], SBC[i]);
+              K[i] = vbfi(m1, Kn[i], K[i]);
+#else
               const uint32_t e01 = pk_eq1(b[i], c[i], one1);
               SBC[i] = pk_mad(e01, sbcv, 0u);
               K[i] = pk_mad(e01, kdv, k0v);
+#endif
             }
           }
         }
       }
+      // keep the per-row registers in place across the branches above (without
+      // this the allocator copies b into a fresh pair every step)
+#pragma unroll
+      for (int i = 0; i < M; ++i) asm volatile("" : "+v"(b[i]), "+v"(SBC[i]), "+v"(K[i]));
       uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
       // Priority 0 for the cell arithmetic, 1 for the send/shift/barrier tail:
       // VALU issue goes by priority then age, so without this the oldest waves
       // of a SIMD finish each step first and idle at the barrier (+3-4 %).
       __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);  // keep the arithmetic between the two
       __builtin_amdgcn_sched_barrier(0);  // keep the arithmetic between the two
       if constexpr (F16)
-        cell_messages_f16<M, SOP>(a, b, c, SBC, K, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx,
+        cell_messages_f16<M, SOP>(a, b, c, SBC, K, DMC, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx,
                              oIy, oIz, oIxy, oIyz, oIxz, oBest);
       else
         cell_messages<M, SOP ? 1 : 0>(a, b, c, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz,
@@ -747,6 +849,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       if (++xpos0 == P) {
         xpos0 = 0;
         binj = b_of_lap(++lap0);
+        row_terms();
       }
       if constexpr (TSA_A_PREFETCH) load_a<M>(a_lane + 4u * (uint32_t)xpos0, a_nx);
 
@@ -901,7 +1004,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
 
   const int32_t y = L * NW + w + 1;  // this wave's DP row
   const uint32_t bw = y <= lb ? (SYM0 << (seqs[o1 + y - 1] & 3)) * 0x00010001u : 0u;
-  uint32_t b[M], c[M], SBC[M], K[M];
+  uint32_t b[M], c[M], SBC[M], K[M], DMC[M];
   uint32_t oIx[M], shIz[M], svIxy[M], svIyz[M], shIxz[2][M], svM[2][M];
   {
     uint32_t one1 = 0x00010001u, sbcv = pa.h_sbc, kdv = pa.h_kd, k0v = pa.h_k0;
@@ -913,6 +1016,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
       const uint32_t c0 = k0 < zt_q ? SYM0 << (seqs[oc + k0] & 3) : 0u;
       const uint32_t c1 = k1 < zt_q ? SYM0 << (seqs[oc + k1] & 3) : 0u;
       c[i] = c0 | (c1 << 16);
+      DMC[i] = dm_over_code(pa.dmf, c[i]);
       b[i] = bw;  // one row per wave
       const uint32_t e01 = pk_eq1(bw, c[i], one1);
       SBC[i] = pk_mad(e01, sbcv, 0u);
@@ -1054,7 +1158,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);  // keep the arithmetic between the two
     if constexpr (F16)
-      cell_messages_f16<M, SOP>(a, b, c, SBC, K, Q, pa, inIx, inIy, inIz, inIxy, inIyz, inIxz,
+      cell_messages_f16<M, SOP>(a, b, c, SBC, K, DMC, Q, pa, inIx, inIy, inIz, inIxy, inIyz, inIxz,
                                 inM, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
     else
       cell_messages<M, SOP ? 1 : 0>(a, b, c, Q, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM,
@@ -1225,6 +1329,7 @@ static PencilArgs make_args(const KParams &kp, bool f16) {
   a.f_pair = pkh(fp + mm);
   const int32_t dm = kp.match - mm, d0 = kp.s3_ab - kp.s3_ne, d1 = kp.s3_eq - kp.s3_ab;
   a.h_dm = pkh(dm * 8192.0);
+  a.dmf = (float)dm;
   a.h_c3 = pkh((double)kp.s3_ne);
   a.h_sbc = pkh((double)dm);  // SBC = e01 * bits(dm), e01 in {0, 1}
   const uint32_t k0 = a.sop ? pkh(3.0 * mm) : pkh(d0 * 8192.0);

@@ -6,11 +6,12 @@ set -e
 cd "$(dirname "$0")/.."
 NAME=$1; DEFS=$2
 PKG=hw-accelerator-three-sequence-alignment_amd
+SRC=${SRC:-$PKG}  # source tree (e.g. a git archive of an older commit)
 OUT=scratch/$NAME
 rm -rf "$OUT"; mkdir -p "$OUT/lib" "$OUT/build"
 cp $PKG/*.py "$OUT/"
 objs=()
-for f in $PKG/csrc/*.hip; do
+for f in $SRC/csrc/*.hip; do
   o="$OUT/build/$(basename "${f%.hip}").o"
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function \
     -DTSA_GIT_DESCRIBE="\"variant-$NAME\"" $DEFS -c "$f" -o "$o" &

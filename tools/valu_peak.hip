@@ -1,0 +1,103 @@
+// valu_peak.hip -- measures the VALU issue ceiling the pencil kernel is priced
+// against: wave64 instructions per cycle per SIMD for the instruction kinds of
+// its step (v_pk_maximum3_f16, v_pk_add_f16, v_bfi_b32, DPP mov), with 1, 2, 4
+// and 8 waves per SIMD, independent chains (8 accumulators per wave).
+//   hipcc -O3 --offload-arch=gfx950 tools/valu_peak.hip -o tools/valu_peak && tools/valu_peak
+// Prints one JSON line per (op, waves/SIMD): G wave-instr/s over the chip and
+// instructions per cycle per SIMD at the measured in-kernel clock.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CHK(x)                                                                  \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+constexpr int ITERS = 4096;  // loop trips; 8 rounds of 8 accumulators each per trip
+
+template <int OP>
+__global__ void valu_loop(unsigned *out, unsigned seed, unsigned long long *clk) {
+  unsigned v0 = seed ^ threadIdx.x, v1 = v0 + 1, v2 = v0 + 2, v3 = v0 + 3, v4 = v0 + 4,
+           v5 = v0 + 5, v6 = v0 + 6, v7 = v0 + 7, k = seed * 3u;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+  for (int it = 0; it < ITERS; ++it) {
+#define BODY(I)                                                                               \
+  if constexpr (OP == 0)                                                                      \
+    asm volatile("v_pk_maximum3_f16 %0, %0, %1, %0" : "+v"(v##I) : "v"(k));                  \
+  else if constexpr (OP == 1)                                                                 \
+    asm volatile("v_pk_add_f16 %0, %0, %1" : "+v"(v##I) : "v"(k));                           \
+  else if constexpr (OP == 2)                                                                 \
+    asm volatile("v_bfi_b32 %0, %1, %0, %1" : "+v"(v##I) : "v"(k));                          \
+  else                                                                                        \
+    asm volatile("v_mov_b32_dpp %0, %0 wave_ror:1 row_mask:0xf bank_mask:0xf" : "+v"(v##I));
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      BODY(0) BODY(1) BODY(2) BODY(3) BODY(4) BODY(5) BODY(6) BODY(7)
+    }
+#undef BODY
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  out[blockIdx.x * blockDim.x + threadIdx.x] = v0 ^ v1 ^ v2 ^ v3 ^ v4 ^ v5 ^ v6 ^ v7;
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    clk[0] = t1 - t0;
+    clk[1] = r1 - r0;
+  }
+}
+
+template <int OP>
+static void run(const char *name, int waves_per_simd, int cus) {
+  const int threads = 256 * (waves_per_simd < 4 ? waves_per_simd : 4);  // <= 1024 per WG
+  const int wgs_per_cu = waves_per_simd <= 4 ? 1 : waves_per_simd / 4;
+  const int grid = cus * wgs_per_cu;
+  unsigned *out;
+  unsigned long long *clk;
+  CHK(hipMalloc(&out, (size_t)grid * threads * 4));
+  CHK(hipMalloc(&clk, 16));
+  hipLaunchKernelGGL(valu_loop<OP>, dim3(grid), dim3(threads), 0, 0, out, 7u, clk);
+  CHK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CHK(hipEventCreate(&e0));
+  CHK(hipEventCreate(&e1));
+  const int reps = 5;
+  CHK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL(valu_loop<OP>, dim3(grid), dim3(threads), 0, 0, out, 7u + r, clk);
+  CHK(hipEventRecord(e1));
+  CHK(hipEventSynchronize(e1));
+  float ms = 0;
+  CHK(hipEventElapsedTime(&ms, e0, e1));
+  unsigned long long hclk[2];
+  CHK(hipMemcpy(hclk, clk, 16, hipMemcpyDeviceToHost));
+  const double ghz = hclk[1] ? (double)hclk[0] / (double)hclk[1] * 0.1 : 0.0;  // memrealtime 100 MHz
+  const double waves = (double)grid * threads / 64.0;
+  const double instr = waves * ITERS * 64.0 * reps;  // wave-instructions
+  const double rate = instr / (ms * 1e-3);
+  const double per_simd_cycle = ghz > 0 ? rate / (cus * 4.0) / (ghz * 1e9) : 0.0;
+  printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"G_wave_instr_per_s\": %.1f, \"clock_ghz\": %.3f, "
+         "\"instr_per_cycle_per_simd\": %.3f}\n",
+         name, waves_per_simd, rate / 1e9, ghz, per_simd_cycle);
+  CHK(hipFree(out));
+  CHK(hipFree(clk));
+}
+
+int main() {
+  hipDeviceProp_t prop;
+  CHK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+  for (int w : {1, 2, 4, 8}) {
+    run<0>("v_pk_maximum3_f16", w, cus);
+    run<1>("v_pk_add_f16", w, cus);
+    run<2>("v_bfi_b32", w, cus);
+    run<3>("v_mov_b32_dpp", w, cus);
+  }
+  return 0;
+}
