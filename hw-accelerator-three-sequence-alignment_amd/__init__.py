@@ -59,8 +59,13 @@ SYMBOLS = {"A": 0, "T": 1, "C": 2, "G": 3, "N": 4}
 EXPORTS = (
     "tsa_default_params", "tsa_validate", "tsa_score_gpu", "tsa_score_gpu_ex",
     "tsa_score_batch", "tsa_batch_workspace_size", "tsa_score_batch_async",
-    "tsa_device_count", "tsa_strerror", "tsa_version", "tsa_describe_plan",
+    "tsa_device_count", "tsa_strerror", "tsa_version", "tsa_describe_plan", "tsa_align_gpu",
 )
+
+# Alignment columns (tsa_align_gpu): the state of each column and which of
+# (A, B, C) it consumes -- the predecessor offsets of src/PE_1cyc.v:164-218.
+MOVES = ("M", "Ix", "Iy", "Iz", "Ixy", "Iyz", "Ixz")
+MOVE_CONSUMES = ((1, 1, 1), (1, 0, 0), (0, 1, 0), (0, 0, 1), (1, 1, 0), (0, 1, 1), (1, 0, 1))
 
 
 class TsaParams(ctypes.Structure):
@@ -121,6 +126,8 @@ def _load_lib() -> ctypes.CDLL:
                                           ctypes.c_size_t, ctypes.c_void_p]
     lib.tsa_describe_plan.argtypes = [ctypes.c_int32] * 4 + [pp, ctypes.c_int32, ctypes.c_int32,
                                                             ctypes.c_char_p, ctypes.c_size_t]
+    lib.tsa_align_gpu.argtypes = [u8p, ctypes.c_int32, u8p, ctypes.c_int32, u8p, ctypes.c_int32,
+                                  pp, i32p, u8p, ctypes.c_int32, i32p, i32p, ctypes.c_int32]
     lib.tsa_device_count.argtypes = []
     lib.tsa_strerror.argtypes = [ctypes.c_int]
     lib.tsa_strerror.restype = ctypes.c_char_p
@@ -128,7 +135,7 @@ def _load_lib() -> ctypes.CDLL:
     lib.tsa_version.restype = ctypes.c_char_p
     for name in ("tsa_validate", "tsa_score_gpu", "tsa_score_gpu_ex", "tsa_score_batch",
                  "tsa_batch_workspace_size", "tsa_score_batch_async", "tsa_device_count",
-                 "tsa_describe_plan"):
+                 "tsa_describe_plan", "tsa_align_gpu"):
         getattr(lib, name).restype = ctypes.c_int
     return lib
 
@@ -196,6 +203,91 @@ def score(a, b, c, params: Optional[TsaParams] = None, kernel: str | int = "auto
     if final_states:
         return int(out.value), tuple(int(v) for v in fin)
     return int(out.value)
+
+
+def align(a, b, c, params: Optional[TsaParams] = None, device: int = 0):
+    """Optimal alignment of one triple (tsa_align_gpu): ``(score, start, moves)``.
+
+    ``moves`` holds one state index per alignment column in forward order
+    (``MOVES`` names them, ``MOVE_CONSUMES`` says which sequences each
+    consumes); ``start`` = (x0, y0, z0), the symbols of A, B, C before the path
+    (free start at the zero faces). An extension: the reference's
+    alignment-output ports are commented out (src/TriAlign_tb.sv:239-260)."""
+    p = params or TsaParams.default()
+    A, B, C = _as_u8(a), _as_u8(b), _as_u8(c)
+    cap = len(A) + len(B) + len(C)
+    mv = np.zeros(max(cap, 1), dtype=np.uint8)
+    sc, n = ctypes.c_int32(0), ctypes.c_int32(0)
+    st = (ctypes.c_int32 * 3)()
+    rc = _lib.tsa_align_gpu(_ptr(A, ctypes.c_uint8), len(A), _ptr(B, ctypes.c_uint8), len(B),
+                            _ptr(C, ctypes.c_uint8), len(C), ctypes.byref(p), ctypes.byref(sc),
+                            _ptr(mv, ctypes.c_uint8), cap, ctypes.byref(n), st, device)
+    _check(rc, "tsa_align_gpu")
+    return int(sc.value), tuple(int(v) for v in st), mv[: n.value].copy()
+
+
+def penalty_table(params: Optional[TsaParams] = None):
+    """P[target][source] of src/PE_1cyc.v:164-218 (target/source order MOVES)."""
+    p = params or TsaParams.default()
+    GO, GE = p.gap_open, p.gap_extend
+    GO2, GE2, GOGE = 2 * GO, 2 * GE, GO + GE
+    return ((0, 0, 0, 0, 0, 0, 0),
+            (GO2, GE2, GOGE, GOGE, GOGE, GO2, GOGE),
+            (GO2, GOGE, GE2, GOGE, GOGE, GOGE, GO2),
+            (GO2, GOGE, GOGE, GE2, GO2, GOGE, GOGE),
+            (GO, GE, GE, GO, GE, GO, GO),
+            (GO, GO, GE, GE, GO, GE, GO),
+            (GO, GE, GO, GE, GO, GO, GE))
+
+
+def path_score(a, b, c, start, moves, params: Optional[TsaParams] = None) -> int:
+    """Score of an alignment path re-added transition by transition (no
+    SCORE_BITS wrap): the first column leaves the zero face, every later one
+    pays P[state][previous state] and adds its pair/triple score
+    (src/PE_1cyc.v:159-218). Equals the DP score whenever nothing wraps."""
+    p = params or TsaParams.default()
+    A, B, C = _as_u8(a), _as_u8(b), _as_u8(c)
+    P = penalty_table(p)
+
+    def s2(u, v):
+        return p.match if (u & 3) == (v & 3) else p.mismatch
+
+    def s3(u, v, w):
+        if p.s3_mode == S3_SOP:
+            return s2(u, v) + s2(v, w) + s2(u, w)
+        u, v, w = u & 3, v & 3, w & 3
+        if u == v:
+            return 3 * p.match if v == w else 2 * (p.match + p.mismatch)
+        return 3 * p.mismatch
+
+    x, y, z = start
+    total, prev = 0, None
+    for t in moves:
+        dx, dy, dz = MOVE_CONSUMES[t]
+        x, y, z = x + dx, y + dy, z + dz
+        ax, by, cz = int(A[x - 1]), int(B[y - 1]), int(C[z - 1])
+        add = (s3(ax, by, cz) if t == 0 else s2(ax, by) if t == 4 else s2(by, cz) if t == 5
+               else s2(ax, cz) if t == 6 else 0)
+        total += add - (min(P[t]) if prev is None else P[t][prev])
+        prev = t
+    return total
+
+
+def render_alignment(a, b, c, start, moves) -> tuple[str, str, str]:
+    """The three rows of an alignment (symbols A,T,C,G,N; '-' = gap), from
+    the first aligned column on."""
+    A, B, C = _as_u8(a), _as_u8(b), _as_u8(c)
+    letters = "ATCGN"
+    pos = list(start)
+    rows = ([], [], [])
+    for t in moves:
+        for k, (seq, d) in enumerate(zip((A, B, C), MOVE_CONSUMES[t])):
+            if d:
+                rows[k].append(letters[int(seq[pos[k]])])
+                pos[k] += 1
+            else:
+                rows[k].append("-")
+    return tuple("".join(r) for r in rows)
 
 
 def pack_batch(triples: Iterable[Sequence]) -> tuple[np.ndarray, np.ndarray]:

@@ -16,6 +16,13 @@
 //
 // This kernel is the exact path for every parameter set and length (the
 // pencil kernel's factored arithmetic is exact only when nothing wraps).
+//
+// Traceback (tsa_align_gpu, an extension: the reference's alignment-output
+// ports are commented out, src/TriAlign_tb.sv:239-260): the TB instantiation
+// also stores, per cell, which source state won each of the 7 MAX7s (3 bits
+// each, lowest state index on ties) in a pointer cube tb[y][x+z][z] -- for a
+// wave (fixed y and q, consecutive z) x+z is fixed, so the stores coalesce --
+// and tb_walk follows the pointers back from cell (LA,LB,LC).
 
 #include "tsa_internal.h"
 
@@ -52,23 +59,39 @@ __global__ __launch_bounds__(256) void plane_face_init(int16_t *__restrict__ ws,
 
 __device__ __forceinline__ int32_t wrapv(int32_t v, int32_t sh) { return (v << sh) >> sh; }
 
-// Literal MAX7 of one target: max_s wrap(pred[s] - pen[s] + add).
-template <int T>
+// Literal MAX7 of one target: max_s wrap(pred[s] - pen[s] + add). With TB,
+// arg receives the lowest source index achieving it.
+template <int T, bool TB>
 __device__ __forceinline__ int32_t max7_literal(const int32_t (&pr)[7], const KParams &kp,
-                                               int32_t add, int32_t sh) {
+                                               int32_t add, int32_t sh, uint32_t &arg) {
   int32_t m = wrapv(pr[0] - kp.pen[T][0] + add, sh);
+  uint32_t a = 0;
 #pragma unroll
-  for (int s = 1; s < 7; ++s) m = max(m, wrapv(pr[s] - kp.pen[T][s] + add, sh));
+  for (int s = 1; s < 7; ++s) {
+    const int32_t v = wrapv(pr[s] - kp.pen[T][s] + add, sh);
+    if constexpr (TB) {
+      if (v > m) a = s;
+    }
+    m = max(m, v);
+  }
+  arg = a;
   return m;
+}
+
+// Traceback pointer cube index of cell (x,y,z), 1-based: [y-1][x+z-2][z-1].
+__host__ __device__ inline int64_t tb_index(int32_t x, int32_t y, int32_t z, int32_t la,
+                                            int32_t lc) {
+  return ((int64_t)(y - 1) * (la + lc - 1) + (x + z - 2)) * lc + (z - 1);
 }
 
 // One launch = plane q of every triple (blockIdx.z). Thread (j, r) of block
 // (bx, by) owns row y = ylo + 4*by + r and column z = zlo(y) + 64*bx + j; the
 // 64 lanes of a wave read 64 consecutive z of each predecessor row.
+template <bool TB>
 __global__ __launch_bounds__(256) void plane_step_kernel(
     const uint8_t *__restrict__ seqs, const int64_t *__restrict__ offs, int32_t q,
     int16_t *__restrict__ ws, PlaneLayout L, KParams kp, int32_t *__restrict__ scores,
-    int32_t *__restrict__ final7) {
+    int32_t *__restrict__ final7, uint32_t *__restrict__ tb) {
   const int64_t t = blockIdx.z;
   const int64_t o0 = offs[3 * t], o1 = offs[3 * t + 1], o2 = offs[3 * t + 2], o3 = offs[3 * t + 3];
   const int32_t la = (int32_t)(o1 - o0), lb = (int32_t)(o2 - o1), lc = (int32_t)(o3 - o2);
@@ -117,15 +140,22 @@ __global__ __launch_bounds__(256) void plane_step_kernel(
   else s3 = (a == b) ? ((b == c) ? kp.s3_eq : kp.s3_ab) : kp.s3_ne;
 
   int32_t S[7];
-  S[SM] = max7_literal<SM>(pM, kp, s3, sh);
-  S[SIX] = max7_literal<SIX>(pX, kp, 0, sh);
-  S[SIY] = max7_literal<SIY>(pY, kp, 0, sh);
-  S[SIZ] = max7_literal<SIZ>(pZ, kp, 0, sh);
-  S[SIXY] = max7_literal<SIXY>(pXY, kp, sab, sh);
-  S[SIYZ] = max7_literal<SIYZ>(pYZ, kp, sbc, sh);
-  S[SIXZ] = max7_literal<SIXZ>(pXZ, kp, sac, sh);
+  uint32_t g[7];
+  S[SM] = max7_literal<SM, TB>(pM, kp, s3, sh, g[SM]);
+  S[SIX] = max7_literal<SIX, TB>(pX, kp, 0, sh, g[SIX]);
+  S[SIY] = max7_literal<SIY, TB>(pY, kp, 0, sh, g[SIY]);
+  S[SIZ] = max7_literal<SIZ, TB>(pZ, kp, 0, sh, g[SIZ]);
+  S[SIXY] = max7_literal<SIXY, TB>(pXY, kp, sab, sh, g[SIXY]);
+  S[SIYZ] = max7_literal<SIYZ, TB>(pYZ, kp, sbc, sh, g[SIYZ]);
+  S[SIXZ] = max7_literal<SIXZ, TB>(pXZ, kp, sac, sh, g[SIXZ]);
 #pragma unroll
   for (int s = 0; s < NSTATE; ++s) out[s * P] = (int16_t)S[s];
+  if constexpr (TB) {  // one triple per traceback launch
+    uint32_t w = 0;
+#pragma unroll
+    for (int s = 0; s < NSTATE; ++s) w |= g[s] << (3 * s);
+    tb[tb_index(x, y, z, la, lc)] = w;
+  }
 
   if (x == la && y == lb && z == lc) {  // FINAL_MAX, src/TriAlign_1cyc.v:141-142
     int32_t m = S[0];
@@ -139,12 +169,51 @@ __global__ __launch_bounds__(256) void plane_step_kernel(
   }
 }
 
+// Follow the pointers back from cell (la,lb,lc) (single thread; <= la+lb+lc
+// dependent loads). moves[] gets the states from the end backwards; info =
+// {moves, x0, y0, z0} where (x0,y0,z0) is the face cell the path leaves.
+__global__ void tb_walk(const uint32_t *__restrict__ tb, const int32_t *__restrict__ final7,
+                        int32_t la, int32_t lb, int32_t lc, uint8_t *__restrict__ moves,
+                        int32_t *__restrict__ info) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  // final MAX7 (src/TriAlign_1cyc.v:141-142): lowest state index on ties
+  int32_t T = 0;
+  for (int s = 1; s < NSTATE; ++s)
+    if (final7[s] > final7[T]) T = s;
+  constexpr int DX[7] = {1, 1, 0, 0, 1, 0, 1}, DY[7] = {1, 0, 1, 0, 1, 1, 0},
+                DZ[7] = {1, 0, 0, 1, 0, 1, 1};  // predecessor offsets per state
+  int32_t x = la, y = lb, z = lc, n = 0;
+  for (;;) {
+    moves[n++] = (uint8_t)T;
+    const int32_t px = x - DX[T], py = y - DY[T], pz = z - DZ[T];
+    if (px == 0 || py == 0 || pz == 0 || n >= la + lb + lc) {
+      x = px;
+      y = py;
+      z = pz;
+      break;
+    }
+    T = (int32_t)((tb[tb_index(x, y, z, la, lc)] >> (3 * T)) & 7u);
+    x = px;
+    y = py;
+    z = pz;
+  }
+  info[0] = n;
+  info[1] = x;
+  info[2] = y;
+  info[3] = z;
+}
+
+size_t tb_cube_bytes(int32_t la, int32_t lb, int32_t lc) {
+  return (size_t)lb * (size_t)(la + lc - 1) * (size_t)lc * sizeof(uint32_t);
+}
+
 int plane_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                        int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
                        int32_t *d_scores, int32_t *d_final7, void *d_ws, size_t ws_bytes,
-                       hipStream_t stream) {
+                       hipStream_t stream, uint32_t *d_tb) {
   if (n <= 0) return TSA_OK;
   if (n > 65535) return TSA_EINVAL;  // grid.z limit; callers chunk
+  if (d_tb && n != 1) return TSA_EINVAL;  // traceback: one triple, exact lengths
   if (ws_bytes < plane_workspace_bytes(n, max_la, max_lb, max_lc)) return TSA_ENOMEM;
   const PlaneLayout L = plane_layout(max_lb, max_lc);
   int16_t *ws = (int16_t *)d_ws;
@@ -155,8 +224,12 @@ int plane_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t 
   for (int32_t q = 2; q <= qmax; ++q) {
     const int32_t rows = (max_lb < q - 1 ? max_lb : q - 1);
     const dim3 grid((wmax + 63) / 64, (rows + 3) / 4, n);
-    hipLaunchKernelGGL(plane_step_kernel, grid, block, 0, stream, d_seqs, d_offsets, q, ws, L,
-                       kp, d_scores, d_final7);
+    if (d_tb)
+      hipLaunchKernelGGL(plane_step_kernel<true>, grid, block, 0, stream, d_seqs, d_offsets, q, ws,
+                         L, kp, d_scores, d_final7, d_tb);
+    else
+      hipLaunchKernelGGL(plane_step_kernel<false>, grid, block, 0, stream, d_seqs, d_offsets, q,
+                         ws, L, kp, d_scores, d_final7, nullptr);
   }
   return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
 }

@@ -343,6 +343,76 @@ int tsa_score_batch(const uint8_t *seqs, const int64_t *offsets, int32_t n, cons
   return TSA_OK;
 }
 
+int tsa_align_gpu(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb, const uint8_t *c,
+                  int32_t lc, const tsa_params *p, int32_t *score, uint8_t *moves, int32_t max_moves,
+                  int32_t *n_moves, int32_t *start, int32_t device) {
+  if (!score || !moves || !n_moves || !start) return TSA_EINVAL;
+  int rc = tsa_validate(a, la, b, lb, c, lc, p);
+  if (rc) return rc;
+  if ((int64_t)max_moves < (int64_t)la + lb + lc) return TSA_EINVAL;
+  const int nd = tsa_device_count();
+  if (nd <= 0) return TSA_ENODEV;
+  if (device < 0 || device >= nd) return TSA_ENODEV;
+  KParams kp;
+  if ((rc = build_kparams(p, &kp))) return rc;
+  const int64_t len = (int64_t)la + lb + lc;
+  const int64_t off[4] = {0, la, (int64_t)la + lb, len};
+  const size_t ws_bytes = plane_workspace_bytes(1, la, lb, lc);
+  const size_t tb_bytes = tb_cube_bytes(la, lb, lc);
+  uint8_t *d_seqs = nullptr, *d_moves = nullptr;
+  int64_t *d_off = nullptr;
+  int32_t *d_small = nullptr;  // [0] score, [1..7] final states, [8..11] walk info
+  uint32_t *d_tb = nullptr;
+  void *d_ws = nullptr;
+  hipStream_t s = nullptr;
+  int32_t h_small[12];
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  if (hipMalloc(&d_seqs, len) != hipSuccess || hipMalloc(&d_off, sizeof(off)) != hipSuccess ||
+      hipMalloc(&d_small, sizeof(h_small)) != hipSuccess ||
+      hipMalloc(&d_moves, (size_t)len) != hipSuccess ||
+      hipMalloc(&d_ws, std::max<size_t>(ws_bytes, 16)) != hipSuccess ||
+      hipMalloc(&d_tb, std::max<size_t>(tb_bytes, 16)) != hipSuccess) {
+    rc = TSA_ENOMEM;
+    goto done;
+  }
+  HIPCHK(hipMemcpyAsync(d_seqs, a, la, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d_seqs + la, b, lb, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d_seqs + la + lb, c, lc, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d_off, off, sizeof(off), hipMemcpyHostToDevice, s));
+  rc = plane_launch_batch(d_seqs, d_off, 1, la, lb, lc, kp, d_small, d_small + 1, d_ws, ws_bytes,
+                          s, d_tb);
+  if (rc) goto done;
+  hipLaunchKernelGGL(tb_walk, dim3(1), dim3(64), 0, s, d_tb, d_small + 1, la, lb, lc, d_moves,
+                     d_small + 8);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(h_small, d_small, sizeof(h_small), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (h_small[8] < 1 || h_small[8] > len) {
+    rc = TSA_EINTERNAL;
+    goto done;
+  }
+  {
+    std::vector<uint8_t> rev((size_t)h_small[8]);
+    HIPCHK(hipMemcpy(rev.data(), d_moves, rev.size(), hipMemcpyDeviceToHost));
+    for (size_t k = 0; k < rev.size(); ++k) moves[k] = rev[rev.size() - 1 - k];
+  }
+  *score = h_small[0];
+  *n_moves = h_small[8];
+  start[0] = h_small[9];
+  start[1] = h_small[10];
+  start[2] = h_small[11];
+done:
+  if (d_seqs) (void)hipFree(d_seqs);
+  if (d_off) (void)hipFree(d_off);
+  if (d_small) (void)hipFree(d_small);
+  if (d_moves) (void)hipFree(d_moves);
+  if (d_ws) (void)hipFree(d_ws);
+  if (d_tb) (void)hipFree(d_tb);
+  if (s) (void)hipStreamDestroy(s);
+  return rc;
+}
+
 int tsa_describe_plan(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
                       const tsa_params *p, int32_t kernel, int32_t sync, char *buf, size_t len) {
   if (!buf || len == 0 || n < 1 || max_la < 1 || max_lb < 1 || max_lc < 1 || !params_ok(p))

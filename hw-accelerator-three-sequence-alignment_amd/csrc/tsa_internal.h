@@ -51,6 +51,10 @@ size_t plane_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t 
 int plane_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                        int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
                        int32_t *d_scores, int32_t *d_final7, void *d_ws, size_t ws_bytes,
-                       hipStream_t stream);
+                       hipStream_t stream, uint32_t *d_tb = nullptr);
+// Traceback: pointer cube of one (la,lb,lc) triple and the walk kernel.
+size_t tb_cube_bytes(int32_t la, int32_t lb, int32_t lc);
+__global__ void tb_walk(const uint32_t *tb, const int32_t *final7, int32_t la, int32_t lb,
+                        int32_t lc, uint8_t *moves, int32_t *info);
 
 }  // namespace tsa

@@ -23,6 +23,8 @@
  *   (no reference equivalent: the reference    tsa_score_batch_async(): device
  *    has one alignment in flight)                 pointers + caller stream, for
  *                                                 in-HBM throughput runs
+ *   alignment-output ports (commented out,     tsa_align_gpu(): the optimal path
+ *    src/TriAlign_tb.sv:239-260)                  as alignment columns
  *
  * Conventions
  *   - Symbols are one byte each, 0..4 = A,T,C,G,N (src/TriAlign_tb.sv:42-46).
@@ -115,6 +117,32 @@ int tsa_score_batch_async(const uint8_t *d_seqs, const int64_t *d_offsets,
                           int32_t max_lc, const tsa_params *p, int32_t kernel,
                           int32_t *d_scores, void *d_workspace,
                           size_t workspace_bytes, void *stream);
+
+/* Optimal alignment of one triple (synchronous, HIP device `device`): the
+ * path behind the score, as one move per alignment column. This has no RTL
+ * counterpart -- the testbench's alignment-output ports are commented out
+ * (src/TriAlign_tb.sv:239-260) -- so it is an extension, defined by the same
+ * recurrence (src/PE_1cyc.v:164-218) and computed by the literal PLANE
+ * arithmetic. moves[k], k < *n_moves, in forward order, is the state of the
+ * k-th column, which says which sequences it consumes:
+ *   TSA_MOVE_M (a,b,c) _IX (a) _IY (b) _IZ (c) _IXY (a,b) _IYZ (b,c) _IXZ (a,c).
+ * start[3] receives the face cell (x0,y0,z0) the path leaves: the zero faces
+ * make the start free, so symbols before a[x0], b[y0], c[z0] are not aligned
+ * (0-based: the first aligned symbols are a[x0], b[y0], c[z0] as consumed).
+ * Ties go to the lowest state index, at the final MAX7 and at every cell.
+ * max_moves must be >= la + lb + lc. The pointer cube needs 4*lb*(la+lc-1)*lc
+ * bytes of device memory (TSA_ENOMEM when it cannot be allocated). */
+#define TSA_MOVE_M 0
+#define TSA_MOVE_IX 1
+#define TSA_MOVE_IY 2
+#define TSA_MOVE_IZ 3
+#define TSA_MOVE_IXY 4
+#define TSA_MOVE_IYZ 5
+#define TSA_MOVE_IXZ 6
+int tsa_align_gpu(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
+                  const uint8_t *c, int32_t lc, const tsa_params *p, int32_t *score,
+                  uint8_t *moves, int32_t max_moves, int32_t *n_moves, int32_t *start,
+                  int32_t device);
 
 /* Which kernel, arithmetic and schedule a batch of these sizes would run, as a
  * short text such as "pencil lap f16 rtl M=1 NW=16 laps=16 tiles=1 waves=1"

@@ -60,6 +60,8 @@ def lib() -> ctypes.CDLL:
         L.tsao_rtl_run.argtypes = three + [ctypes.c_int32, i32p, i32p,
                                            ctypes.POINTER(ctypes.c_int64)]
         L.tsao_rtl_run.restype = ctypes.c_int
+        L.tsao_align.argtypes = three + [pp, i32p, u8p, ctypes.c_int32, i32p, i32p]
+        L.tsao_align.restype = ctypes.c_int
         L.tsao_gen_uniform.argtypes = [ctypes.c_uint64, u8p, ctypes.c_int32]
         L.tsao_gen_uniform.restype = None
         L.tsao_now.argtypes = []
@@ -95,6 +97,23 @@ def score(a, b, c, params: OracleParams | None = None, method: str = "xplane",
     if final_states:
         return int(out.value), tuple(int(v) for v in fin)
     return int(out.value)
+
+
+def align(a, b, c, params: OracleParams | None = None):
+    """Traceback of the literal form: (score, (x0, y0, z0), moves) with moves
+    the state index of each alignment column in forward order."""
+    p = params or default_params()
+    A, B, C = _u8(a), _u8(b), _u8(c)
+    cap = len(A) + len(B) + len(C)
+    mv = np.zeros(cap, dtype=np.uint8)
+    sc, n = ctypes.c_int32(0), ctypes.c_int32(0)
+    st = (ctypes.c_int32 * 3)()
+    rc = lib().tsao_align(_p(A, ctypes.c_uint8), len(A), _p(B, ctypes.c_uint8), len(B),
+                          _p(C, ctypes.c_uint8), len(C), ctypes.byref(p), ctypes.byref(sc),
+                          _p(mv, ctypes.c_uint8), cap, ctypes.byref(n), st)
+    if rc:
+        raise ValueError(f"oracle rc={rc}")
+    return int(sc.value), tuple(int(v) for v in st), mv[: n.value].copy()
 
 
 def state_range(a, b, c, params: OracleParams | None = None) -> tuple[int, int]:

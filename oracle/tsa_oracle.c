@@ -228,6 +228,74 @@ int tsao_score_diag(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
   return TSA_OK;
 }
 
+/* ---- traceback (extension; no RTL counterpart) ------------------------------
+ * The path behind the score: the whole cube of literal (wrapped) states is
+ * kept, then walked back from (la,lb,lc), recomputing each state's 7 wrapped
+ * candidates and taking the lowest source index that achieves it (the final
+ * MAX7 likewise). Moves are state indices, forward order; start = the face
+ * cell the path leaves. Independent of the GPU's pointer cube by design. */
+int tsao_align(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb, const uint8_t *c,
+               int32_t lc, const tsa_params *p, int32_t *score, uint8_t *moves,
+               int32_t max_moves, int32_t *n_moves, int32_t *start) {
+  int rc = check_args(a, la, b, lb, c, lc, p);
+  if (rc) return rc;
+  if (!score || !moves || !n_moves || !start) return TSA_EINVAL;
+  if ((int64_t)max_moves < (int64_t)la + lb + lc) return TSA_EINVAL;
+  const int bits = p->score_bits;
+  int32_t P[7][7];
+  tsao_penalty_table(p, P);
+  const size_t W = (size_t)lc + 1, H = (size_t)lb + 1, D = (size_t)la + 1;
+  if (D * H * W > ((size_t)1 << 26)) return TSA_ENOMEM; /* test sizes only */
+  int32_t *cube = (int32_t *)calloc(D * H * W * 7, sizeof(int32_t)); /* faces stay 0 */
+  if (!cube) return TSA_ENOMEM;
+#define CELL(x, y, z) (cube + (((size_t)(x) * H + (size_t)(y)) * W + (size_t)(z)) * 7)
+  for (int32_t x = 1; x <= la; ++x)
+    for (int32_t y = 1; y <= lb; ++y)
+      for (int32_t z = 1; z <= lc; ++z) {
+        const int ax = a[x - 1] & 3, by = b[y - 1] & 3, cz = c[z - 1] & 3;
+        cell_literal(CELL(x - 1, y - 1, z - 1), CELL(x - 1, y, z), CELL(x, y - 1, z),
+                     CELL(x, y, z - 1), CELL(x - 1, y - 1, z), CELL(x, y - 1, z - 1),
+                     CELL(x - 1, y, z - 1), wrapv(tsao_s3(ax, by, cz, p), bits),
+                     wrapv(tsao_s2(ax, by, p), bits), wrapv(tsao_s2(by, cz, p), bits),
+                     wrapv(tsao_s2(ax, cz, p), bits), P, bits, CELL(x, y, z));
+      }
+  static const int DX[7] = {1, 1, 0, 0, 1, 0, 1}, DY[7] = {1, 0, 1, 0, 1, 1, 0},
+                   DZ[7] = {1, 0, 0, 1, 0, 1, 1};
+  const int32_t *fin = CELL(la, lb, lc);
+  int T = 0;
+  for (int s = 1; s < 7; ++s) if (fin[s] > fin[T]) T = s;
+  *score = fin[T];
+  int32_t x = la, y = lb, z = lc, n = 0;
+  for (;;) {
+    moves[n++] = (uint8_t)T;
+    const int32_t px = x - DX[T], py = y - DY[T], pz = z - DZ[T];
+    if (px == 0 || py == 0 || pz == 0) { x = px; y = py; z = pz; break; }
+    const int ax = a[x - 1] & 3, by = b[y - 1] & 3, cz = c[z - 1] & 3;
+    int32_t add = 0;
+    if (T == TSAO_M) add = wrapv(tsao_s3(ax, by, cz, p), bits);
+    else if (T == TSAO_IXY) add = wrapv(tsao_s2(ax, by, p), bits);
+    else if (T == TSAO_IYZ) add = wrapv(tsao_s2(by, cz, p), bits);
+    else if (T == TSAO_IXZ) add = wrapv(tsao_s2(ax, cz, p), bits);
+    const int32_t *pr = CELL(px, py, pz), target = CELL(x, y, z)[T];
+    int src = -1;
+    for (int s = 0; s < 7 && src < 0; ++s)
+      if (wrapv((int64_t)pr[s] - P[T][s] + add, bits) == target) src = s;
+    if (src < 0) { free(cube); return TSA_EINTERNAL; }
+    x = px; y = py; z = pz;
+    T = src;
+  }
+#undef CELL
+  for (int32_t k = 0; k < n / 2; ++k) { /* forward order */
+    const uint8_t t = moves[k];
+    moves[k] = moves[n - 1 - k];
+    moves[n - 1 - k] = t;
+  }
+  *n_moves = n;
+  start[0] = x; start[1] = y; start[2] = z;
+  free(cube);
+  return TSA_OK;
+}
+
 /* ---- factored message form ------------------------------------------------
  * A cell with states S sends to each successor target T the value
  *   msg_T = max_s (S[s] - P[T][s]);

@@ -61,6 +61,14 @@ int tsao_score_msg(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
                    const uint8_t *c, int32_t lc, const tsa_params *p,
                    int32_t *score);
 
+/* Traceback of the literal form (extension: the RTL outputs only the score):
+ * moves[] = state index per alignment column, forward order; start = face
+ * cell the path leaves; ties to the lowest state index. Cubes up to 2^26
+ * cells (full state cube in memory). Mirrors tsa_align_gpu's contract. */
+int tsao_align(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb, const uint8_t *c,
+               int32_t lc, const tsa_params *p, int32_t *score, uint8_t *moves,
+               int32_t max_moves, int32_t *n_moves, int32_t *start);
+
 /* Min / max over every state value of the cube (unbounded arithmetic), for
  * range checks of the int16 GPU state storage. */
 int tsao_state_range(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,

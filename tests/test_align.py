@@ -1,0 +1,104 @@
+"""Traceback (tsa_align_gpu) -- an extension of the score path: the reference's
+alignment-output ports are commented out (src/TriAlign_tb.sv:239-260), so no
+reference output pins it. Pinned instead by (1) the oracle's independent
+traceback (full state cube, candidates recomputed at every cell) agreeing with
+the GPU's pointer-cube walk move for move, (2) the path re-scored transition by
+transition equalling the DP score, (3) the testbench input's analytic path
+(all-A n^3 -> n M columns from (0,0,0))."""
+import numpy as np
+import pytest
+
+
+def _check_path(tsa, a, b, c, score, start, moves, params=None, rescore=True):
+    la, lb, lc = len(a), len(b), len(c)
+    assert min(start) == 0 and all(v >= 0 for v in start)          # leaves a zero face
+    used = np.sum([tsa.MOVE_CONSUMES[t] for t in moves], axis=0)
+    assert tuple(int(v) for v in np.asarray(start) + used) == (la, lb, lc)  # ends at (LA,LB,LC)
+    if rescore:
+        assert tsa.path_score(a, b, c, start, moves, params) == score
+
+
+def test_oracle_align_testbench_input(tsa, orc):
+    for n in (8, 24, 64):
+        z = [0] * n
+        s, st, mv = orc.align(z, z, z)
+        assert s == 3 * n and st == (0, 0, 0) and list(mv) == [0] * n
+
+
+def test_oracle_align_dat_triple(tsa, orc, golden):
+    dat = next(c for c in golden if c["name"] == "dat")
+    s, st, mv = orc.align(dat["a"], dat["b"], dat["c"])
+    assert s == dat["score"] == 1
+    _check_path(tsa, dat["a"], dat["b"], dat["c"], s, st, mv)
+    rows = tsa.render_alignment(dat["a"], dat["b"], dat["c"], st, mv)
+    assert len({len(r) for r in rows}) == 1 and len(rows[0]) == len(mv)
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(s3_mode=1), dict(score_bits=0),
+                                dict(match=2, mismatch=-3, gap_open=5, gap_extend=2, score_bits=0),
+                                dict(gap_open=1, gap_extend=2, score_bits=0)])
+def test_oracle_align_rescores(tsa, orc, kw):
+    rng = np.random.default_rng(len(kw) * 7 + kw.get("s3_mode", 0))
+    op, tp = orc.default_params(**kw), tsa.TsaParams.default(**kw)
+    for _ in range(15):
+        la, lb, lc = (int(v) for v in rng.integers(1, 30, 3))
+        a, b, c = (rng.integers(0, 5, n).astype(np.uint8) for n in (la, lb, lc))
+        s, st, mv = orc.align(a, b, c, op)
+        assert s == orc.score(a, b, c, op)
+        _check_path(tsa, a, b, c, s, st, mv, tp)
+
+
+def test_oracle_align_wrapped_path_is_consistent(tsa, orc):
+    # SCORE_BITS 6: candidates wrap, so the re-added path score need not equal
+    # the wrapped DP score, but the path is still a valid walk ending at the cube corner
+    rng = np.random.default_rng(3)
+    op = orc.default_params(score_bits=6)
+    z = np.zeros(40, np.uint8)
+    s, st, mv = orc.align(z, z, z, op)
+    assert s == orc.score(z, z, z, op)
+    _check_path(tsa, z, z, z, s, st, mv, rescore=False)
+    a, b, c = (rng.integers(0, 4, 35).astype(np.uint8) for _ in range(3))
+    s, st, mv = orc.align(a, b, c, op)
+    _check_path(tsa, a, b, c, s, st, mv, rescore=False)
+
+
+@pytest.mark.gpu
+def test_gpu_align_matches_oracle(gpu, orc, golden):
+    used = 0
+    for c in golden:
+        if len(c["a"]) * len(c["b"]) * len(c["c"]) > 200 ** 3:
+            continue
+        p, op = gpu.TsaParams.default(**c["params"]), orc.default_params(**c["params"])
+        got = gpu.align(c["a"], c["b"], c["c"], p)
+        ref = orc.align(c["a"], c["b"], c["c"], op)
+        assert got[0] == ref[0] == c["score"] and got[1] == ref[1], c["name"]
+        assert np.array_equal(got[2], ref[2]), c["name"]
+        used += 1
+    assert used >= 30
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(), dict(s3_mode=1), dict(score_bits=0), dict(score_bits=6),
+                                dict(match=3, mismatch=-1, gap_open=2, gap_extend=2, score_bits=16)])
+def test_gpu_align_random(gpu, orc, kw):
+    rng = np.random.default_rng(100 + len(kw))
+    p, op = gpu.TsaParams.default(**kw), orc.default_params(**kw)
+    for _ in range(8):
+        la, lb, lc = (int(v) for v in rng.integers(1, 90, 3))
+        a, b, c = (rng.integers(0, 5, n).astype(np.uint8) for n in (la, lb, lc))
+        got, ref = gpu.align(a, b, c, p), orc.align(a, b, c, op)
+        assert got[0] == ref[0] and got[1] == ref[1] and np.array_equal(got[2], ref[2]), (la, lb, lc)
+        _check_path(gpu, a, b, c, got[0], got[1], got[2], p, rescore=kw.get("score_bits") != 6)
+
+
+@pytest.mark.gpu
+def test_gpu_align_256_cube(gpu, orc, synth):
+    # configs[2] size: the pointer cube is 4*256*511*256 B = 134 MB of HBM; the
+    # path must re-score to the kernel's score (12-bit wrap cannot occur here)
+    a, b, c = synth.triple(0, 256)
+    s, st, mv = gpu.align(a, b, c)
+    assert s == gpu.score(a, b, c)
+    _check_path(gpu, a, b, c, s, st, mv)
+    z = np.zeros(256, np.uint8)
+    s, st, mv = gpu.align(z, z, z)
+    assert s == 768 and st == (0, 0, 0) and len(mv) == 256 and not mv.any()
