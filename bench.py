@@ -203,13 +203,15 @@ def main():
                                   prm, args.kernel)
         sstep()
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
+        times = []  # median of individually timed calls (a latency, not a throughput)
         for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
             sstep()
-        e1.record(stream)
-        torch.cuda.synchronize()
-        sms = e0.elapsed_time(e1) / reps
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1))
+        sms = float(np.median(times))
         return {"ms": round(sms, 4), "gcups": round(Ls ** 3 / (sms * 1e-3) / 1e9, 3),
                 "score": int(s_score.item()), "score_bits": prm.score_bits}
 
@@ -220,7 +222,7 @@ def main():
         if not args.no_extra_configs:
             other_configs["configs[1]: one 64^3 triple"] = time_single(64, params, reps=10)
             other_configs["configs[3]: one 1024^3 triple"] = time_single(
-                1024, tsa.TsaParams.default(score_bits=16), reps=3)
+                1024, tsa.TsaParams.default(score_bits=16), reps=7)
     except Exception as e:  # noqa: BLE001
         log("single-cube measurement failed:", e)
 
