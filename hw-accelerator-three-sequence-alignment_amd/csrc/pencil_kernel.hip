@@ -565,10 +565,10 @@ __device__ __forceinline__ uint32_t lane_half_mask(int32_t ls, int32_t hs, uint3
 // Position k -> (lane, register, half) of the layout above.
 template <int M>
 __device__ __forceinline__ void pos_split(int32_t k, int32_t &l, int32_t &i, int32_t &h) {
-  h = k >= 64 * M;
-  const int32_t r = k - h * 64 * M;
-  l = r / M;
-  i = r % M;
+  const uint32_t u = (uint32_t)k;  // k >= 0: shifts and masks only (M is a power of 2)
+  h = (int32_t)(u / (64u * M));
+  l = (int32_t)((u / M) & 63u);
+  i = (int32_t)(u % M);
 }
 
 // The step lambdas are left to the regular inliner for M <= 2 (an early forced
@@ -713,9 +713,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     // One step; PH = t & 1 picks the register roles and the LDS record slots,
     // ROLE the wave's place in the lap (0: wave 0, reads the ring; 2: the last
     // wave, writes it; 1: the others), so the loop body has no role branches.
-    auto step = [&](auto ph, auto role, int32_t t) {
+    auto step = [&](auto ph, auto role, int32_t t, auto fin_step) {
       constexpr int PH = decltype(ph)::value;
       constexpr int ROLE = decltype(role)::value;
+      constexpr bool FIN = decltype(fin_step)::value;  // the last step (t == T-1)
       // this step's A codes (LDS table) and the B code of position x = 1
       uint32_t a[M];
       if constexpr (TSA_A_PREFETCH) {
@@ -801,9 +802,11 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     __builtin_amdgcn_s_setprio(1);
       // ---- the final cell (src/TriAlign_1cyc.v:141-142,342-345) is in wave w_f's
       // last step; it is read back after the loop
-      if (t == T - 1 && w == w_f) {
+      if constexpr (FIN) {
+        if (w == w_f) {
 #pragma unroll
-        for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
+          for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
+        }
       }
 
       // ---- send this step's record to the wave below (or the ring)
@@ -868,14 +871,26 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     };
 
+    // the last step is peeled off (it records the final cell), so the loop
+    // body carries no final-step test; PH stays t & 1
     auto run = [&](auto role) {
       int32_t t = 0;
+      const int32_t T1 = T - 1;
+      constexpr std::integral_constant<int, 0> P0{};
+      constexpr std::integral_constant<int, 1> P1{};
+      constexpr std::false_type mid{};
+      constexpr std::true_type last{};
 #pragma unroll 1
-      for (; t + 1 < T; t += 2) {
-        TSA_INLINE_IF_WIDE(step(std::integral_constant<int, 0>{}, role, t));
-        TSA_INLINE_IF_WIDE(step(std::integral_constant<int, 1>{}, role, t + 1));
+      for (; t + 1 < T1; t += 2) {
+        TSA_INLINE_IF_WIDE(step(P0, role, t, mid));
+        TSA_INLINE_IF_WIDE(step(P1, role, t + 1, mid));
       }
-      if (t < T) TSA_INLINE_IF_WIDE(step(std::integral_constant<int, 0>{}, role, t));
+      if (t < T1) {
+        TSA_INLINE_IF_WIDE(step(P0, role, t, mid));
+        TSA_INLINE_IF_WIDE(step(P1, role, t + 1, last));
+      } else {
+        TSA_INLINE_IF_WIDE(step(P0, role, t, last));
+      }
     };
     if (w == 0) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 0>{}));
     else if (w == NW - 1) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 2>{}));
@@ -1087,9 +1102,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
 
   // ROLE (wave 0): bit 0 = rows of lap L-1 arrive (L > 0), bit 2 = z records of
   // tile q-1 arrive (q > 0); 2 = middle waves; 3 = the last wave
-  auto step = [&](auto ph, auto role, int32_t t) {
+  auto step = [&](auto ph, auto role, int32_t t, auto fin_step) {
     constexpr int PH = decltype(ph)::value;
     constexpr int ROLE = decltype(role)::value;
+    constexpr bool FIN = decltype(fin_step)::value;  // the last step (t == T-1)
     constexpr bool W0 = ROLE == 0 || ROLE == 1 || ROLE == 4 || ROLE == 5;
     constexpr bool YIN = ROLE == 1 || ROLE == 5, ZIN0 = ROLE == 4 || ROLE == 5;
     uint32_t a[M];
@@ -1165,9 +1181,11 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
                                     nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    if (final_wg && t == T - 1 && w == w_f) {
+    if constexpr (FIN) {
+      if (final_wg && w == w_f) {
 #pragma unroll
-      for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
+        for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
+      }
     }
     // z staging: this wave's last position, and (wave 0) the row above's
     if (zout && lane == 63) {
@@ -1235,14 +1253,24 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
-  auto run = [&](auto role) {
+  auto run = [&](auto role) {  // last step peeled, as in the helix kernel
     int32_t t = 0;
+    const int32_t T1 = T - 1;
+    constexpr std::integral_constant<int, 0> P0{};
+    constexpr std::integral_constant<int, 1> P1{};
+    constexpr std::false_type mid{};
+    constexpr std::true_type last{};
 #pragma unroll 1
-    for (; t + 1 < T; t += 2) {
-      TSA_INLINE_IF_WIDE(step(std::integral_constant<int, 0>{}, role, t));
-      TSA_INLINE_IF_WIDE(step(std::integral_constant<int, 1>{}, role, t + 1));
+    for (; t + 1 < T1; t += 2) {
+      TSA_INLINE_IF_WIDE(step(P0, role, t, mid));
+      TSA_INLINE_IF_WIDE(step(P1, role, t + 1, mid));
     }
-    if (t < T) TSA_INLINE_IF_WIDE(step(std::integral_constant<int, 0>{}, role, t));
+    if (t < T1) {
+      TSA_INLINE_IF_WIDE(step(P0, role, t, mid));
+      TSA_INLINE_IF_WIDE(step(P1, role, t + 1, last));
+    } else {
+      TSA_INLINE_IF_WIDE(step(P0, role, t, last));
+    }
   };
   if (w == 0) {
     if (L == 0) {
