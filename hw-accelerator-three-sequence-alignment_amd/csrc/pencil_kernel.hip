@@ -88,6 +88,12 @@ constexpr int REC_BYTES = 16;      // {Iy, Ixy, Iyz, best} packed pairs per lane
 #ifndef TSA_ROW_NEXT   // next row's per-row terms precomputed once per lap
 #define TSA_ROW_NEXT 1
 #endif
+#ifndef TSA_PIN_ROW    // pin the per-row registers after the x = 1 block
+#define TSA_PIN_ROW 1
+#endif
+#ifndef TSA_SCHED_FENCE  // sched_barrier fences around the helix cell arithmetic
+#define TSA_SCHED_FENCE 1
+#endif
 constexpr int RING_EXTRA = 8;
 
 // Packed (both halves) constants. int16 form: two's complement; exact-f16 form
@@ -782,14 +788,16 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       }
       // keep the per-row registers in place across the branches above (without
       // this the allocator copies b into a fresh pair every step)
+#if TSA_PIN_ROW
 #pragma unroll
       for (int i = 0; i < M; ++i) asm volatile("" : "+v"(b[i]), "+v"(SBC[i]), "+v"(K[i]));
+#endif
       uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
       // Priority 0 for the cell arithmetic, 1 for the send/shift/barrier tail:
       // VALU issue goes by priority then age, so without this the oldest waves
       // of a SIMD finish each step first and idle at the barrier (+3-4 %).
       __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);  // keep the arithmetic between the two
+      if constexpr (TSA_SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);  // keep the arithmetic between the two
       if constexpr (F16)
         cell_messages_f16<M, SOP>(a, b, c, SBC, K, DMC, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx,
                              oIy, oIz, oIxy, oIyz, oIxz, oBest);
@@ -797,9 +805,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         cell_messages<M, SOP ? 1 : 0>(a, b, c, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz,
                                       inM, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
 
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
+      if constexpr (TSA_SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
       // ---- the final cell (src/TriAlign_1cyc.v:141-142,342-345) is in wave w_f's
       // last step; it is read back after the loop
       if constexpr (FIN) {
@@ -1180,7 +1187,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_lap_kernel(
       cell_messages<M, SOP ? 1 : 0>(a, b, c, Q, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM,
                                     nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
     if constexpr (FIN) {
       if (final_wg && w == w_f) {
 #pragma unroll
