@@ -102,3 +102,21 @@ def test_gpu_align_256_cube(gpu, orc, synth):
     z = np.zeros(256, np.uint8)
     s, st, mv = gpu.align(z, z, z)
     assert s == 768 and st == (0, 0, 0) and len(mv) == 256 and not mv.any()
+
+
+@pytest.mark.gpu
+def test_cli_align(gpu, golden, tmp_path):
+    import os
+    import subprocess
+    dat = next(c for c in golden if c["name"] == "dat")
+    for k in "abc":
+        (tmp_path / f"{k}.dat").write_text("\r\n".join(str(v) for v in dat[k]) + "\r\n")
+    cli = os.path.join(os.path.dirname(gpu.LIB_PATH), "..", "bin", "tsa")
+    r = subprocess.run([cli] + [str(tmp_path / f"{k}.dat") for k in "abc"] + ["--align"],
+                       capture_output=True, text=True, check=True)
+    lines = r.stdout.strip().splitlines()
+    assert lines[0].split()[-1] == "1"
+    score, start, moves = gpu.align(dat["a"], dat["b"], dat["c"])
+    rows = gpu.render_alignment(dat["a"], dat["b"], dat["c"], start, moves)
+    assert [ln.split()[1] for ln in lines[2:5]] == list(rows)
+    assert f"({start[0]},{start[1]},{start[2]})" in lines[1]
