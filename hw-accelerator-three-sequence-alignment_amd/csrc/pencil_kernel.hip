@@ -114,6 +114,7 @@ struct PencilGeom {
   int32_t M;        // pairs per lane
   int32_t P;        // lap period (steps)
   int32_t R;        // ring rows
+  bool two;         // two triples per workgroup (LC <= 64, M = 1)
   int64_t ring_bytes_per_triple;
 };
 
@@ -130,17 +131,26 @@ static int helix_nw(int M) {
   if (const char *e = getenv("TSA_PENCIL_NW")) return atoi(e) == 16 ? 16 : 8;  // tuning knob
   return PENCIL_NW_DEFAULT;
 }
+// TWO: for LC <= 64 a wave's two 16-bit halves hold two different triples at
+// the same 64 positions (a lane = one z of both), instead of positions k and
+// k+64 of one triple -- no idle half, and the lap period shrinks to max(LA, 64).
+static bool helix_two(int32_t max_lc) {
+  if (const char *e = getenv("TSA_PENCIL_TWO")) return atoi(e) != 0 && max_lc <= 64;  // A/B knob
+  return max_lc <= 64;
+}
 static PencilGeom pencil_geom(int32_t max_la, int32_t max_lc) {
   PencilGeom g;
   g.M = pencil_pairs(max_lc);
-  g.P = std::max(max_la, 128 * g.M);  // >= 128 > NW + helix_pd + STORE_SLACK: ring lag
+  // >= 64 > NW + helix_pd + STORE_SLACK: ring lag
+  g.two = helix_two(max_lc);
+  g.P = std::max(max_la, g.two ? 64 : 128 * g.M);
   g.R = g.P + RING_EXTRA;
   g.ring_bytes_per_triple = (int64_t)g.R * g.M * 64 * REC_BYTES;
   return g;
 }
 static size_t helix_lds(int M, int NW, int32_t P, int32_t max_lb) {
   return (size_t)(NW - 1) * 2 * M * 1024 + (size_t)helix_pd(M) * M * 1024 +
-         4 * ((size_t)P + 128 * M) + 4 * (((size_t)max_lb + 3) & ~(size_t)3) + (size_t)M * 256;
+         4 * ((size_t)P + 128 * M) + 4 * (((size_t)max_lb + 3) & ~(size_t)3) + (size_t)M * 512;
 }
 
 // The factored messages widen each target's highest-penalty group to all seven
@@ -222,7 +232,8 @@ static double helix_est(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_l
   const int64_t per_cu = std::max<int64_t>(
       1, std::min<int64_t>(LDS_MAX / helix_lds(g.M, nw, g.P, max_lb), waves_per_cu(g.M) / nw));
   const double T = (double)((max_lb - 1) / nw) * g.P + max_la + nw + max_lc;
-  return (double)((n + 256 * per_cu - 1) / (256 * per_cu)) * T * step_cost(g.M);
+  const int64_t units = g.two ? (n + 1) / 2 : n;
+  return (double)((units + 256 * per_cu - 1) / (256 * per_cu)) * T * step_cost(g.M);
 }
 
 // The lap kernel's geometry if it should run, else .ok = false (helix).
@@ -597,7 +608,7 @@ __device__ __forceinline__ void pos_split(int32_t k, int32_t &l, int32_t &i, int
 //        sB  [LB] u32              B code, both halves
 //        fin [M][64] u32           best of the final step (wave w_f)
 // F16 selects the exact-f16 arithmetic above, else the int16 form.
-template <int M, int NW, bool F16, bool SOP>
+template <int M, int NW, bool F16, bool SOP, bool TWO>
 __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restrict__ seqs,
                                                          const int64_t *__restrict__ offs,
                                                          int32_t n, int32_t P, int32_t R,
@@ -619,34 +630,53 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t sel = lane == 0 ? 0x05040302u : 0x07060504u;
+  static_assert(!TWO || M == 1, "two triples per wave: 64 positions, M = 1");
+  // TWO: the halves are two triples at the same position, so lane 0 takes its
+  // whole word from the z = 0 face (no half crosses from lane 63)
+  const uint32_t sel = lane == 0 ? (TWO ? 0x03020100u : 0x05040302u) : 0x07060504u;
+  constexpr int KS = TWO ? 64 : 128 * M;  // positions (per half in TWO)
   uint32_t ones = F16 ? 0x08000800u : 0x00010001u;  // f16: match indicator 2^-13
   asm volatile("" : "+v"(ones));                     // keep it in a VGPR (VOP3P operand)
   const PencilArgs pv = F16 ? pa : pin_score_consts(pa);
   uint32_t fsv = pa.f_single, fpv = pa.f_pair;  // VGPR copies for v_bfi_b32 / v_pk_mad_u16
   uint32_t sbcv = pa.h_sbc, kdv = pa.h_kd, k0v = pa.h_k0, one1 = 0x00010001u;
-  uint32_t hmLo = 0x0000FFFFu, hmHi = 0xFFFF0000u, zero = 0u;
+  uint32_t hmLo = TWO ? 0xFFFFFFFFu : 0x0000FFFFu, hmHi = 0xFFFF0000u, zero = 0u;
   asm volatile("" : "+v"(fsv), "+v"(fpv), "+v"(sbcv), "+v"(kdv), "+v"(k0v), "+v"(one1));
   asm volatile("" : "+v"(hmLo), "+v"(hmHi), "+v"(zero));
   // a[i] of this lane at step t is sA2[(t-w) mod P + ZT - M lane - i]
   const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
                           4u * (uint32_t)(ZT - M * lane - (M - 1));
 
-  for (int tri = blockIdx.x; tri < n; tri += gridDim.x) {
+  const int32_t nunit = TWO ? (n + 1) / 2 : n;  // workgroup units: triples, or pairs
+  for (int unit = blockIdx.x; unit < nunit; unit += gridDim.x) {
+    const int tri = TWO ? 2 * unit : unit;
     const int64_t o0 = offs[3 * (int64_t)tri], o1 = offs[3 * (int64_t)tri + 1];
     const int64_t o2 = offs[3 * (int64_t)tri + 2], o3 = offs[3 * (int64_t)tri + 3];
     const int32_t la = (int32_t)(o1 - o0), lb = (int32_t)(o2 - o1), lc = (int32_t)(o3 - o2);
+    // TWO: the high halves score triple tri+1 (or repeat tri when n is odd)
+    const bool has1 = TWO && tri + 1 < n;
+    const int64_t *of1 = offs + 3 * (int64_t)(has1 ? tri + 1 : tri);
+    const int64_t q0 = of1[0], q1 = of1[1], q2 = of1[2];
+    const int32_t la1 = TWO ? (int32_t)(q1 - q0) : la, lb1 = TWO ? (int32_t)(q2 - q1) : lb;
+    const int32_t lc1 = TWO ? (int32_t)(of1[3] - q2) : lc;
+    const int32_t lbm = max(lb, lb1);
     uint8_t *ring = ring_base + (int64_t)blockIdx.x * ring_stride;
 
-    // ---- stage A codes (padded to P, halves k/k+64M) and B; face records in the ring
+    // ---- stage A codes (padded to P, halves k/k+64M or, TWO, the two triples) and
+    // B; face records in the ring
     for (int j = threadIdx.x; j < P + ZT; j += 64 * NW) {
-      const int x0 = ((j - ZT) % P + P) % P, x1 = ((j - ZT - 64 * M) % P + P) % P;
+      const int x0 = ((j - ZT) % P + P) % P, x1 = TWO ? x0 : ((j - ZT - 64 * M) % P + P) % P;
       const uint32_t c0 = x0 < la ? SYM0 << (seqs[o0 + x0] & 3) : 0u;
-      const uint32_t c1 = x1 < la ? SYM0 << (seqs[o0 + x1] & 3) : 0u;
+      const uint32_t c1 = x1 < la1 ? SYM0 << (seqs[(TWO ? q0 : o0) + x1] & 3) : 0u;
       sA2[j] = c0 | (c1 << 16);
     }
-    for (int i = threadIdx.x; i < lb; i += 64 * NW)
-      sB[i] = (SYM0 << (seqs[o1 + i] & 3)) * 0x00010001u;
+    for (int i = threadIdx.x; i < lbm; i += 64 * NW) {
+      if constexpr (TWO)
+        sB[i] = (i < lb ? SYM0 << (seqs[o1 + i] & 3) : 0u) |
+                ((i < lb1 ? SYM0 << (seqs[q1 + i] & 3) : 0u) << 16);
+      else
+        sB[i] = (SYM0 << (seqs[o1 + i] & 3)) * 0x00010001u;
+    }
     {
       const uint4 face = make_uint4(pa.f_single, pa.f_pair, pa.f_pair, 0u);
       const int64_t n16 = (int64_t)R * M * 64;
@@ -660,9 +690,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     uint32_t oIx[M], shIz[M], svIxy[M], svIyz[M], shIxz[2][M], svM[2][M];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
-      const int k0 = M * lane + i, k1 = 64 * M + M * lane + i;
+      const int k0 = M * lane + i, k1 = TWO ? k0 : 64 * M + M * lane + i;
       const uint32_t c0 = k0 < lc ? SYM0 << (seqs[o2 + k0] & 3) : 0u;
-      const uint32_t c1 = k1 < lc ? SYM0 << (seqs[o2 + k1] & 3) : 0u;
+      const uint32_t c1 = k1 < lc1 ? SYM0 << (seqs[(TWO ? q2 : o2) + k1] & 3) : 0u;
       c[i] = c0 | (c1 << 16);
       DMC[i] = dm_over_code(pa.dmf, c[i]);
       b[i] = SBC[i] = K[i] = 0;  // set when a position reaches x = 1 of its lap
@@ -678,7 +708,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     // B code of row lap0*NW+w+1, taken by the position at x = 1 (0 past LB)
     auto b_of_lap = [&](int32_t lp) -> uint32_t {
       const int32_t r = lp * NW + w;
-      return (lp >= 0 && r < lb) ? sB[r] : 0u;
+      return (lp >= 0 && r < lbm) ? sB[r] : 0u;
     };
     uint32_t binj = b_of_lap(lap0);
     // the per-row terms of the row whose B code is binj, for every position:
@@ -697,7 +727,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     row_terms();
     const int32_t lap_f = (lb - 1) / NW, w_f = (lb - 1) % NW, k_f = lc - 1;
     const int32_t t_f = lap_f * P + (la - 1) + w_f + k_f;  // final cell (la, lb, lc)
-    const int32_t T = t_f + 1;
+    // TWO: the high-half triple's final cell, captured by its own step test
+    const int32_t w_f1 = (lb1 - 1) % NW, k_f1 = lc1 - 1;
+    const int32_t t_f1 = ((lb1 - 1) / NW) * P + (la1 - 1) + w_f1 + k_f1;
+    const int32_t T = (TWO ? max(t_f, t_f1) : t_f) + 1;
 
     // wave 0: prime the LDS-DMA pipeline (ring row of step s = s - P + NW - 1)
     const int32_t lag = P - (NW - 1);
@@ -757,13 +790,13 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       // ---- x == 1 at position k* = (t - w) mod P: its x-1 inputs are the x = 0
       // face (EN_i==1&&EN==0 gating, src/PE_1cyc.v:164-178,196-202,212-218), and
       // it starts row lap0*NW+w+1, whose B symbol it takes here.
-      if (xpos0 < ZT) {
+      if (xpos0 < KS) {
         int32_t ls, is, hs;
         pos_split<M>(xpos0, ls, is, hs);
 #if TSA_LANE_MASK
         const uint32_t m1 = lane_half_mask(ls, hs, hmLo, hmHi);
 #else
-        const uint32_t m1 = lane == ls ? (hs ? 0xFFFF0000u : 0x0000FFFFu) : 0u;
+        const uint32_t m1 = lane == ls ? (TWO ? 0xFFFFFFFFu : hs ? 0xFFFF0000u : 0x0000FFFFu) : 0u;
 #endif
 #pragma unroll
         for (int i = 0; i < M; ++i) {
@@ -809,7 +842,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       __builtin_amdgcn_s_setprio(1);
       // ---- the final cell (src/TriAlign_1cyc.v:141-142,342-345) is in wave w_f's
       // last step; it is read back after the loop
-      if constexpr (FIN) {
+      if constexpr (TWO) {  // two final cells, possibly at different steps
+        if (t == t_f && w == w_f) fin[lane] = oBest[0];
+        if (t == t_f1 && w == w_f1) fin[64 + lane] = oBest[0];
+      } else if constexpr (FIN) {
         if (w == w_f) {
 #pragma unroll
           for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
@@ -830,7 +866,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll
           for (int i = 0; i < M; ++i) {
             const uint32_t m = ((M * lane + i > lim) ? 0x0000FFFFu : 0u) |
-                               ((64 * M + M * lane + i > lim) ? 0xFFFF0000u : 0u);
+                               (((TWO ? 0 : 64 * M) + M * lane + i > lim) ? 0xFFFF0000u : 0u);
             oIy[i] = bfi(m, pa.f_single, oIy[i]);
             oIxy[i] = bfi(m, pa.f_pair, oIxy[i]);
             oIyz[i] = bfi(m, pa.f_pair, oIyz[i]);
@@ -905,11 +941,18 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      int32_t l_f, i_f, h_f;
-      pos_split<M>(k_f, l_f, i_f, h_f);
-      const uint32_t v = fin[i_f * 64 + l_f];
-      const uint16_t hb = (uint16_t)(h_f ? (v >> 16) : (v & 0xFFFF));
-      scores[tri] = F16 ? (int32_t)(float)__builtin_bit_cast(_Float16, hb) : (int32_t)(int16_t)hb;
+      auto decode = [&](uint16_t hb) -> int32_t {
+        return F16 ? (int32_t)(float)__builtin_bit_cast(_Float16, hb) : (int32_t)(int16_t)hb;
+      };
+      if constexpr (TWO) {
+        scores[tri] = decode((uint16_t)(fin[k_f] & 0xFFFF));
+        if (has1) scores[tri + 1] = decode((uint16_t)(fin[64 + k_f1] >> 16));
+      } else {
+        int32_t l_f, i_f, h_f;
+        pos_split<M>(k_f, l_f, i_f, h_f);
+        const uint32_t v = fin[i_f * 64 + l_f];
+        scores[tri] = decode((uint16_t)(h_f ? (v >> 16) : (v & 0xFFFF)));
+      }
     }
     __syncthreads();
   }
@@ -1394,12 +1437,15 @@ static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                     const PencilArgs &pa, hipStream_t stream) {
   const int32_t lds_a = 4 * (g.P + 128 * M), lds_b = 4 * ((max_lb + 3) & ~3);
   const size_t lds = helix_lds(M, NW, g.P, max_lb);
-  auto kfn = pencil_kernel<M, NW, F16, SOP>;
+  // TWO (two triples per workgroup) exactly when pencil_geom sized P for it
+  const bool two = M == 1 && g.two;
+  auto kfn = two ? pencil_kernel<M, NW, F16, SOP, M == 1> : pencil_kernel<M, NW, F16, SOP, false>;
   if (lds > LDS_MAX) return TSA_EINVAL;
   if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
     return TSA_EDEVICE;
-  const int grid = n < 65535 ? n : 65535;
+  const int32_t units = two ? (n + 1) / 2 : n;
+  const int grid = units < 65535 ? units : 65535;
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * NW), lds, stream, d_seqs, d_offsets, n, g.P,
                      g.R, lds_a, lds_b, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores,
                      pa);
@@ -1472,7 +1518,8 @@ void pencil_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, 
     return;
   }
   const PencilGeom g = pencil_geom(max_la, max_lc);
-  snprintf(buf, len, "pencil helix %s %s M=%d NW=%d P=%d", arith, s3, g.M, helix_nw(g.M), g.P);
+  snprintf(buf, len, "pencil helix %s %s M=%d NW=%d P=%d%s", arith, s3, g.M, helix_nw(g.M), g.P,
+           g.two ? " two" : "");
 }
 
 int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,

@@ -334,3 +334,25 @@ def test_1024_cube_config_c4(gpu, orc, synth):
     p, op = gpu.TsaParams.default(score_bits=16), orc.default_params(score_bits=16)
     assert gpu.score(a, b, c, p, kernel="pencil") == orc.score(a, b, c, op)
 
+
+
+@pytest.mark.parametrize("two", ["0", "1"])
+def test_pencil_two_triples_per_wave(gpu, orc, monkeypatch, two):
+    # LC <= 64: a wave's halves hold two different triples (TWO) -- ragged
+    # pairs whose final cells fall in different steps, an odd batch (the last
+    # workgroup scores one triple), LA above and below the 64-step lap period,
+    # f16 and int16, both s3 modes
+    monkeypatch.setenv("TSA_PENCIL_MODE", "helix")
+    monkeypatch.setenv("TSA_PENCIL_TWO", two)
+    rng = np.random.default_rng(80 + int(two))
+    for kw, arith in [(dict(), "f16"), (dict(s3_mode=1), "f16"), (dict(), "i16"),
+                      (dict(match=2, mismatch=-3, gap_open=5, gap_extend=2, score_bits=16), "f16")]:
+        monkeypatch.setenv("TSA_PENCIL_ARITH", arith)
+        triples = []
+        for _ in range(23):
+            la, lb, lc = int(rng.integers(1, 140)), int(rng.integers(1, 70)), int(rng.integers(1, 65))
+            triples.append(tuple(rng.integers(0, 5, n).astype(np.uint8) for n in (la, lb, lc)))
+        seqs, offs = gpu.pack_batch(triples)
+        ref = orc.score_batch(seqs, offs, orc.default_params(**kw), nthreads=8)
+        got = gpu.score_batch(triples, gpu.TsaParams.default(**kw))
+        assert np.array_equal(got, ref), (two, kw, arith)
