@@ -126,3 +126,26 @@ def test_cli_reports_no_device_or_score():
         assert "TriAlign Score:" in r.stdout and r.stdout.split()[-1] == "1"
     else:
         assert "no HIP device" in r.stderr
+
+
+def test_align_argument_checks(tsa):
+    # tsa_align_gpu validates before touching a device: a moves buffer shorter
+    # than la+lb+lc, null outputs and bad symbols are TSA_EINVAL everywhere
+    import ctypes
+    a = np.zeros(4, np.uint8)
+    p = tsa.TsaParams.default()
+    mv = np.zeros(16, np.uint8)
+    sc, n = ctypes.c_int32(0), ctypes.c_int32(0)
+    st = (ctypes.c_int32 * 3)()
+    u8 = lambda x: x.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+    lib = tsa.lib()
+    assert lib.tsa_align_gpu(u8(a), 4, u8(a), 4, u8(a), 4, ctypes.byref(p), ctypes.byref(sc),
+                             u8(mv), 11, ctypes.byref(n), st, 0) == tsa.TSA_EINVAL
+    assert lib.tsa_align_gpu(u8(a), 4, u8(a), 4, u8(a), 4, ctypes.byref(p), None,
+                             u8(mv), 16, ctypes.byref(n), st, 0) == tsa.TSA_EINVAL
+    bad = np.array([0, 9, 1, 2], np.uint8)
+    assert lib.tsa_align_gpu(u8(bad), 4, u8(a), 4, u8(a), 4, ctypes.byref(p), ctypes.byref(sc),
+                             u8(mv), 16, ctypes.byref(n), st, 0) == tsa.TSA_EINVAL
+    # traceback helpers are host-only
+    assert tsa.path_score([0] * 4, [0] * 4, [0] * 4, (0, 0, 0), [0] * 4) == 12
+    assert tsa.render_alignment("ACGT", "AGT", "ACT", (0, 0, 0), [0, 6, 4, 0]) == ("ACGT", "A-GT", "AC-T")
