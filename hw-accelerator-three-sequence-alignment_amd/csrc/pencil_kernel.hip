@@ -91,6 +91,15 @@ constexpr int REC_BYTES = 16;      // {Iy, Ixy, Iyz, best} packed pairs per lane
 #ifndef TSA_PIN_ROW    // pin the per-row registers after the x = 1 block
 #define TSA_PIN_ROW 1
 #endif
+#ifndef TSA_UNROLL4  // helix loop body of four steps instead of two (M <= 2)
+#define TSA_UNROLL4 1
+#endif
+#ifndef TSA_HM_TRACK  // half mask kept in a register, switched at two events per lap
+#define TSA_HM_TRACK 1
+#endif
+#ifndef TSA_IS_STATIC  // M = 2: the x = 1 register index from the wave parity
+#define TSA_IS_STATIC 1
+#endif
 #ifndef TSA_SCHED_FENCE  // sched_barrier fences around the helix cell arithmetic
 #define TSA_SCHED_FENCE 1
 #endif
@@ -144,6 +153,7 @@ static PencilGeom pencil_geom(int32_t max_la, int32_t max_lc) {
   // >= 64 > NW + helix_pd + STORE_SLACK: ring lag
   g.two = helix_two(max_lc);
   g.P = std::max(max_la, g.two ? 64 : 128 * g.M);
+  g.P = (g.P + g.M - 1) / g.M * g.M;  // even for M = 2: the x = 1 register is PH ^ (w & 1)
   g.R = g.P + RING_EXTRA;
   g.ring_bytes_per_triple = (int64_t)g.R * g.M * 64 * REC_BYTES;
   return g;
@@ -705,6 +715,17 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     // position-0 bookkeeping (wave-uniform): u0 = t - w
     int32_t xpos0 = (P - (w % P)) % P;  // (t - w) mod P at t = 0
     int32_t lap0 = w == 0 ? 0 : -1;     // floor((t - w) / P)
+#if TSA_HM_TRACK
+    // bfi half mask of the x = 1 position xpos0 -- low half below 64M, high
+    // half below KS, none from KS up to the lap wrap (P > KS) -- switched at
+    // those events (one compare per step) rather than tested every step
+    auto hm_of = [&](int32_t xp) -> uint32_t {
+      return xp >= KS ? zero : xp >= 64 * M ? hmHi : hmLo;
+    };
+    auto ev_of = [&](int32_t xp) -> int32_t { return xp < 64 * M ? 64 * M : xp < KS ? KS : P; };
+    uint32_t hmCur = hm_of(xpos0);
+    int32_t next_ev = ev_of(xpos0);
+#endif
     // B code of row lap0*NW+w+1, taken by the position at x = 1 (0 past LB)
     auto b_of_lap = [&](int32_t lp) -> uint32_t {
       const int32_t r = lp * NW + w;
@@ -754,7 +775,11 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     // wave, writes it; 1: the others), so the loop body has no role branches.
     auto step = [&](auto ph, auto role, int32_t t, auto fin_step) {
       constexpr int PH = decltype(ph)::value;
-      constexpr int ROLE = decltype(role)::value;
+      constexpr int ROLE = decltype(role)::value & 3;
+      // M = 2 with even P: the x = 1 position's register (t - w) mod 2 is
+      // PH ^ (w & 1), a compile-time constant for a wave of known parity
+      constexpr int WPAR = (decltype(role)::value >> 2) - 1;  // -1: unknown
+      constexpr int ISC = (M == 2 && WPAR >= 0) ? (PH ^ WPAR) : -1;
       constexpr bool FIN = decltype(fin_step)::value;  // the last step (t == T-1)
       // this step's A codes (LDS table) and the B code of position x = 1
       uint32_t a[M];
@@ -780,7 +805,11 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         inIx[i] = oIx[i];
+#ifdef TSA_EXP_NOREC  // timing experiment only: wrong results
+        inIy[i] = oIx[i] ^ 1u;
+#else
         inIy[i] = rec[i].x;
+#endif
         inIz[i] = shIz[i];
         inIxy[i] = svIxy[i];
         inIyz[i] = svIyz[i];
@@ -790,17 +819,20 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       // ---- x == 1 at position k* = (t - w) mod P: its x-1 inputs are the x = 0
       // face (EN_i==1&&EN==0 gating, src/PE_1cyc.v:164-178,196-202,212-218), and
       // it starts row lap0*NW+w+1, whose B symbol it takes here.
-      if (xpos0 < KS) {
+      if (TSA_HM_TRACK || xpos0 < KS) {  // (tracked: hmCur is 0 past KS)
         int32_t ls, is, hs;
         pos_split<M>(xpos0, ls, is, hs);
-#if TSA_LANE_MASK
+#if TSA_HM_TRACK
+        uint32_t m1;
+        asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(m1) : "v"(hmCur), "s"(1ull << ls));
+#elif TSA_LANE_MASK
         const uint32_t m1 = lane_half_mask(ls, hs, hmLo, hmHi);
 #else
         const uint32_t m1 = lane == ls ? (TWO ? 0xFFFFFFFFu : hs ? 0xFFFF0000u : 0x0000FFFFu) : 0u;
 #endif
 #pragma unroll
         for (int i = 0; i < M; ++i) {
-          if (i == is) {
+          if (ISC >= 0 ? i == ISC : i == is) {
             inIx[i] = vbfi(m1, fsv, inIx[i]);
             inIxy[i] = vbfi(m1, fpv, inIxy[i]);
             inIxz[i] = vbfi(m1, fpv, inIxz[i]);
@@ -892,11 +924,23 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       zshift<M>(svIyz, rz, sel, pa.f_pair);
       zshift<M>(svM[PH], rw, sel, 0u);
       // position 0 advances to u0 + 1
+#if TSA_HM_TRACK
+      if (__builtin_expect(++xpos0 == next_ev, 0)) {
+        if (xpos0 == P) {
+          xpos0 = 0;
+          binj = b_of_lap(++lap0);
+          row_terms();
+        }
+        hmCur = hm_of(xpos0);
+        next_ev = ev_of(xpos0);
+      }
+#else
       if (++xpos0 == P) {
         xpos0 = 0;
         binj = b_of_lap(++lap0);
         row_terms();
       }
+#endif
       if constexpr (TSA_A_PREFETCH) load_a<M>(a_lane + 4u * (uint32_t)xpos0, a_nx);
 
       // ---- wave 0: fetch the record of step t + PD into the slot just consumed
@@ -911,7 +955,11 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         if (++st_row == R) st_row = 0;
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(M * STORE_SLACK) : "memory");
       }
+#ifdef TSA_EXP_NOBAR  // timing experiment only: wrong results
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
     };
 
     // the last step is peeled off (it records the final cell), so the loop
@@ -923,6 +971,15 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       constexpr std::integral_constant<int, 1> P1{};
       constexpr std::false_type mid{};
       constexpr std::true_type last{};
+#if TSA_UNROLL4
+#pragma unroll 1
+      for (; M <= 2 && t + 3 < T1; t += 4) {
+        TSA_INLINE_IF_WIDE(step(P0, role, t, mid));
+        TSA_INLINE_IF_WIDE(step(P1, role, t + 1, mid));
+        TSA_INLINE_IF_WIDE(step(P0, role, t + 2, mid));
+        TSA_INLINE_IF_WIDE(step(P1, role, t + 3, mid));
+      }
+#endif
 #pragma unroll 1
       for (; t + 1 < T1; t += 2) {
         TSA_INLINE_IF_WIDE(step(P0, role, t, mid));
@@ -935,9 +992,13 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         TSA_INLINE_IF_WIDE(step(P0, role, t, last));
       }
     };
-    if (w == 0) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 0>{}));
-    else if (w == NW - 1) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 2>{}));
-    else TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 1>{}));
+    // role | (w & 1) + 1 << 2 (M = 2, see ISC in step)
+    constexpr int W0 = (M == 2 && TSA_IS_STATIC) ? 4 : 0, W1 = (M == 2 && TSA_IS_STATIC) ? 8 : 0;
+    static_assert(NW % 2 == 0, "the last wave is odd");
+    if (w == 0) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 0 + W0>{}));
+    else if (w == NW - 1) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 2 + W1>{}));
+    else if (W0 != 0 && (w & 1)) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 1 + W1>{}));
+    else TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 1 + W0>{}));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
