@@ -88,6 +88,9 @@ def test_describe_plan(tsa):
     assert tsa.describe_plan(1, 256, 256, 256, p).startswith("pencil lap f16 rtl M=1")
     assert "waves=2" in tsa.describe_plan(32, 256, 256, 256, p, sync=True)
     assert tsa.describe_plan(32, 256, 256, 256, p, sync=False).startswith("pencil helix")
+    # M = 2 lap periods are even (the x = 1 register is then PH ^ (w & 1))
+    assert "M=2 NW=8 P=258" in tsa.describe_plan(512, 257, 40, 255, p)
+    assert "M=2 NW=8 P=256" in tsa.describe_plan(512, 255, 40, 255, p)
     p16 = tsa.TsaParams.default(score_bits=16)
     assert tsa.describe_plan(1, 1024, 1024, 1024, p16).startswith("pencil lap i16 rtl")
     sop = tsa.TsaParams.default(s3_mode=tsa.S3_SOP)
