@@ -97,6 +97,11 @@ constexpr int REC_BYTES = 16;      // {Iy, Ixy, Iyz, best} packed pairs per lane
 #ifndef TSA_HM_TRACK  // half mask kept in a register, switched at two events per lap
 #define TSA_HM_TRACK 1
 #endif
+#ifndef TSA_SKEW  // helix: steps between waves; 2 = one barrier per two steps
+#define TSA_SKEW 2
+#endif
+// skew and record slots per wave; M >= 4 keeps skew 1 (twice the slots would not fit LDS)
+__host__ __device__ constexpr int helix_skew(int M) { return M <= 2 ? TSA_SKEW : 1; }
 #ifndef TSA_IS_STATIC  // M = 2: the x = 1 register index from the wave parity
 #define TSA_IS_STATIC 1
 #endif
@@ -159,7 +164,7 @@ static PencilGeom pencil_geom(int32_t max_la, int32_t max_lc) {
   return g;
 }
 static size_t helix_lds(int M, int NW, int32_t P, int32_t max_lb) {
-  return (size_t)(NW - 1) * 2 * M * 1024 + (size_t)helix_pd(M) * M * 1024 +
+  return (size_t)(NW - 1) * 2 * helix_skew(M) * M * 1024 + (size_t)helix_pd(M) * M * 1024 +
          4 * ((size_t)P + 128 * M) + 4 * (((size_t)max_lb + 3) & ~(size_t)3) + (size_t)M * 512;
 }
 
@@ -632,8 +637,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
   constexpr int SLOT_BYTES = M * PAIR_BYTES;
   constexpr int ZT = 128 * M;
   constexpr int PD = helix_pd(M);
+  constexpr int HSK = helix_skew(M), HNSL = 2 * HSK;
   uint8_t *xr = smem;
-  uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT_BYTES;
+  uint8_t *xr0 = xr + (NW - 1) * HNSL * SLOT_BYTES;
   uint32_t *sA2 = (uint32_t *)(xr0 + PD * SLOT_BYTES);
   uint32_t *sB = (uint32_t *)((uint8_t *)sA2 + lds_a);
   uint32_t *fin = (uint32_t *)((uint8_t *)sB + lds_b);
@@ -713,7 +719,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       svM[0][i] = svM[1][i] = 0;
     }
     // position-0 bookkeeping (wave-uniform): u0 = t - w
-    int32_t xpos0 = (P - (w % P)) % P;  // (t - w) mod P at t = 0
+    int32_t xpos0 = (P - ((HSK * w) % P)) % P;  // (t - HSK w) mod P at t = 0
     int32_t lap0 = w == 0 ? 0 : -1;     // floor((t - w) / P)
 #if TSA_HM_TRACK
     // bfi half mask of the x = 1 position xpos0 -- low half below 64M, high
@@ -747,14 +753,14 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     };
     row_terms();
     const int32_t lap_f = (lb - 1) / NW, w_f = (lb - 1) % NW, k_f = lc - 1;
-    const int32_t t_f = lap_f * P + (la - 1) + w_f + k_f;  // final cell (la, lb, lc)
+    const int32_t t_f = lap_f * P + (la - 1) + HSK * w_f + k_f;  // final cell (la, lb, lc)
     // TWO: the high-half triple's final cell, captured by its own step test
     const int32_t w_f1 = (lb1 - 1) % NW, k_f1 = lc1 - 1;
-    const int32_t t_f1 = ((lb1 - 1) / NW) * P + (la1 - 1) + w_f1 + k_f1;
+    const int32_t t_f1 = ((lb1 - 1) / NW) * P + (la1 - 1) + HSK * w_f1 + k_f1;
     const int32_t T = (TWO ? max(t_f, t_f1) : t_f) + 1;
 
     // wave 0: prime the LDS-DMA pipeline (ring row of step s = s - P + NW - 1)
-    const int32_t lag = P - (NW - 1);
+    const int32_t lag = P - HSK * (NW - 1);
     if (w == 0) {
 #pragma unroll 1
       for (int s = 0; s < PD; ++s) {
@@ -774,12 +780,15 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     // ROLE the wave's place in the lap (0: wave 0, reads the ring; 2: the last
     // wave, writes it; 1: the others), so the loop body has no role branches.
     auto step = [&](auto ph, auto role, int32_t t, auto fin_step) {
-      constexpr int PH = decltype(ph)::value;
+      // ph = t & 3 (or -1: slot phase at run time); PH = t & 1 picks the registers
+      constexpr int PQ = decltype(ph)::value;
+      constexpr int PH = PQ & 1;
+      const int32_t q = PQ >= 0 && PQ < 4 ? PQ : (t & 3);  // record slot phase
       constexpr int ROLE = decltype(role)::value & 3;
       // M = 2 with even P: the x = 1 position's register (t - w) mod 2 is
       // PH ^ (w & 1), a compile-time constant for a wave of known parity
       constexpr int WPAR = (decltype(role)::value >> 2) - 1;  // -1: unknown
-      constexpr int ISC = (M == 2 && WPAR >= 0) ? (PH ^ WPAR) : -1;
+      constexpr int ISC = (M == 2 && WPAR >= 0) ? (HSK == 2 ? PH : PH ^ WPAR) : -1;
       constexpr bool FIN = decltype(fin_step)::value;  // the last step (t == T-1)
       // this step's A codes (LDS table) and the B code of position x = 1
       uint32_t a[M];
@@ -797,7 +806,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll
         for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
       } else {
-        const uint8_t *src = xr + ((w - 1) * 2 + (PH ^ 1)) * SLOT_BYTES + lane * REC_BYTES;
+        const uint8_t *src = xr + ((w - 1) * HNSL + (HSK == 2 ? (q + 2) & 3 : PH ^ 1)) * SLOT_BYTES +
+                             lane * REC_BYTES;
 #pragma unroll
         for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
       }
@@ -886,15 +896,15 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 
       // ---- send this step's record to the wave below (or the ring)
       if constexpr (ROLE != 2) {
-        uint8_t *dst = xr + (w * 2 + PH) * SLOT_BYTES + lane * REC_BYTES;
+        uint8_t *dst = xr + (w * HNSL + (HSK == 2 ? q : PH)) * SLOT_BYTES + lane * REC_BYTES;
 #pragma unroll
         for (int i = 0; i < M; ++i)
           lds_write16(dst + i * PAIR_BYTES, make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
       } else {
         // Positions that have not started (u = t - w - k < 0) must publish the
         // y = 0 face: wave 0 reads this row as "row y0-1" during its lap 0.
-        if (t < ZT + NW) {
-          const int32_t lim = t - w;  // position k started iff k <= lim
+        if (t < ZT + HSK * NW) {
+          const int32_t lim = t - HSK * w;  // position k started iff k <= lim
 #pragma unroll
           for (int i = 0; i < M; ++i) {
             const uint32_t m = ((M * lane + i > lim) ? 0x0000FFFFu : 0u) |
@@ -958,7 +968,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #ifdef TSA_EXP_NOBAR  // timing experiment only: wrong results
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #else
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      // skew 2: a wave reads records two steps old, so one barrier per pair of steps
+      if constexpr (HSK == 1 || PH == 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #endif
     };
 
@@ -967,17 +978,22 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     auto run = [&](auto role) {
       int32_t t = 0;
       const int32_t T1 = T - 1;
-      constexpr std::integral_constant<int, 0> P0{};
-      constexpr std::integral_constant<int, 1> P1{};
+      // P0/P1: t & 1 known, the slot phase t & 3 read at run time (values 4, 5)
+      constexpr std::integral_constant<int, 4> P0{};
+      constexpr std::integral_constant<int, 5> P1{};
+      constexpr std::integral_constant<int, 0> Q0{};
+      constexpr std::integral_constant<int, 1> Q1{};
+      constexpr std::integral_constant<int, 2> Q2{};
+      constexpr std::integral_constant<int, 3> Q3{};
       constexpr std::false_type mid{};
       constexpr std::true_type last{};
 #if TSA_UNROLL4
 #pragma unroll 1
-      for (; M <= 2 && t + 3 < T1; t += 4) {
-        TSA_INLINE_IF_WIDE(step(P0, role, t, mid));
-        TSA_INLINE_IF_WIDE(step(P1, role, t + 1, mid));
-        TSA_INLINE_IF_WIDE(step(P0, role, t + 2, mid));
-        TSA_INLINE_IF_WIDE(step(P1, role, t + 3, mid));
+      for (; (M <= 2 || HSK == 2) && t + 3 < T1; t += 4) {
+        TSA_INLINE_IF_WIDE(step(Q0, role, t, mid));
+        TSA_INLINE_IF_WIDE(step(Q1, role, t + 1, mid));
+        TSA_INLINE_IF_WIDE(step(Q2, role, t + 2, mid));
+        TSA_INLINE_IF_WIDE(step(Q3, role, t + 3, mid));
       }
 #endif
 #pragma unroll 1
