@@ -8,7 +8,9 @@ import numpy as np
 PD, PMIN, NW = 8, 48, 16
 
 
-def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False):
+def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, skew=1):
+    # skew: steps between consecutive waves (TSA_SKEW; the kernel uses 2 for
+    # M <= 2): wave w reads wave w-1's record of step t-skew from 2*skew slots
     la, lb, lc = len(a), len(b), len(c)
     M = 1 if lc <= 128 else 2
     ZT = 128 * M
@@ -33,14 +35,14 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False):
     shIxz1 = np.full(shape, f_pair); shIxz2 = np.full(shape, f_pair)
     svIxy = np.full(shape, f_pair); svIyz = np.full(shape, f_pair)
     svM1 = np.zeros(shape, np.int64); svM2 = np.zeros(shape, np.int64)
-    xr = np.zeros((NW, 2, 64, M, 2, 4), np.int64)   # record slots written by wave w
+    xr = np.zeros((NW, 2 * skew, 64, M, 2, 4), np.int64)   # record slots written by wave w
     ring = np.zeros((R, 64, M, 2, 4), np.int64)
     ring[..., 0] = f_single; ring[..., 1] = f_pair; ring[..., 2] = f_pair; ring[..., 3] = 0
-    lap = P - (NW - 1)
-    xpos0 = np.array([(P - (w % P)) % P for w in range(NW)])
+    lap = P - skew * (NW - 1)
+    xpos0 = np.array([(P - (skew * w % P)) % P for w in range(NW)])
     lap0 = np.array([0 if w == 0 else -1 for w in range(NW)])
     lap_f, w_f, k_f = (lb - 1) // NW, (lb - 1) % NW, lc - 1
-    t_f = lap_f * P + (la - 1) + w_f + k_f
+    t_f = lap_f * P + (la - 1) + skew * w_f + k_f
     h_f = k_f // (64 * M); l_f, i_f = divmod(k_f - 64 * M * h_f, M)
     order = np.argsort(k.reshape(-1))  # flat (lane, pair, half) index of position 0, 1, ...
 
@@ -56,7 +58,7 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False):
     for t in range(t_f + 1):
         rec = np.empty((NW, 64, M, 2, 4), np.int64)
         rec[0] = ring[(t - lap) % R]
-        rec[1:] = xr[:-1, (t - 1) & 1]
+        rec[1:] = xr[:-1, (t - skew) % (2 * skew)]
         inIx, inIy, inIz = oIx.copy(), rec[..., 0].copy(), shIz.copy()
         inIxy, inIyz, inIxz, inM = svIxy.copy(), svIyz.copy(), shIxz2.copy(), svM2.copy()
         for w in range(NW):
@@ -86,9 +88,9 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False):
         oIyz = mx(mx.reduce([sY, sZ, sYZ]) - E, best - O)
         oIxz = mx(mx.reduce([sX, sZ, sXZ]) - E, best - O)
         recout = np.stack([oIy, oIxy, oIyz, best], -1)
-        xr[:, t & 1] = recout
+        xr[:, t % (2 * skew)] = recout
         last = recout[NW - 1].copy()
-        unstarted = (t - (NW - 1) - k) < 0          # u < 0: row y0-1 of lap 0 is the y=0 face
+        unstarted = (t - skew * (NW - 1) - k) < 0   # u < 0: row y0-1 of lap 0 is the y=0 face
         last[unstarted] = [f_single, f_pair, f_pair, 0]
         ring[t % R] = last
         if t == t_f:
