@@ -102,6 +102,9 @@ constexpr int REC_BYTES = 16;      // {Iy, Ixy, Iyz, best} packed pairs per lane
 #endif
 // skew and record slots per wave; M >= 4 keeps skew 1 (twice the slots would not fit LDS)
 __host__ __device__ constexpr int helix_skew(int M) { return M <= 2 ? TSA_SKEW : 1; }
+#ifndef TSA_SETPRIO  // helix: priority 0 for the cell arithmetic, 1 for the tail
+#define TSA_SETPRIO 1
+#endif
 #ifndef TSA_IS_STATIC  // M = 2: the x = 1 register index from the wave parity
 #define TSA_IS_STATIC 1
 #endif
@@ -871,7 +874,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       // Priority 0 for the cell arithmetic, 1 for the send/shift/barrier tail:
       // VALU issue goes by priority then age, so without this the oldest waves
       // of a SIMD finish each step first and idle at the barrier (+3-4 %).
-      __builtin_amdgcn_s_setprio(0);
+      if constexpr (TSA_SETPRIO) __builtin_amdgcn_s_setprio(0);
       if constexpr (TSA_SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);  // keep the arithmetic between the two
       if constexpr (F16)
         cell_messages_f16<M, SOP>(a, b, c, SBC, K, DMC, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx,
@@ -881,7 +884,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
                                       inM, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
 
       if constexpr (TSA_SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
+      if constexpr (TSA_SETPRIO) __builtin_amdgcn_s_setprio(1);
       // ---- the final cell (src/TriAlign_1cyc.v:141-142,342-345) is in wave w_f's
       // last step; it is read back after the loop
       if constexpr (TWO) {  // two final cells, possibly at different steps
