@@ -5,26 +5,36 @@
                     [--kernel auto|plane|pencil] [--per-gpu B] [--length L]
 
 Workload (BASELINE.json metric "GCUPS + achieved HBM GB/s, 256^3 cube"):
-  batch  (default) -- configs[4]'s per-GPU shard: B (default 512) independent
-         256^3 synthetic triples per GPU, weak scaling: N GPUs score N*B
+  batch  (default) -- configs[4]: "4096 independent 256^3 triples sharded across
+         8 GPUs", i.e. B = 512 triples per GPU; weak scaling: N GPUs score N*B
          triples, sharded contiguously, one process per GPU; the only
          collective is the RCCL all-gather of the int32 scores.
   single -- configs[2]: one 256^3 triple per GPU (replicas at N>1).
 A "step" is one pass of the hot path over the GPU's batch, inputs already
 resident in HBM. value = cells scored by all ranks / max-over-ranks time.
-The single-cube latency (configs[2]) is always measured on rank 0 and
-reported under "single_cube". Rank 0 checks a sample of the gathered scores
-against the CPU oracle ("parity") and, at N=1, times the oracle on a bounded
-sample of the same workload ("cpu_baseline").
+
+Ranks: under torch.distributed.run (WORLD_SIZE set) this process is one rank
+and --gpus must equal WORLD_SIZE. Started directly with --gpus N > 1, this
+process starts the N rank processes itself (RANK/LOCAL_RANK/WORLD_SIZE set
+before any of them touches the GPU; this parent never does) and exits with
+their status.
+
+Rank 0 also times single cubes (configs[1..3] and the paper's Table III sizes
+128^3 / 512^3, "single_cube"), checks a sample of the gathered scores against
+the CPU oracle ("parity") and, at N=1, times the oracle on a bounded sample of
+the same workload on every host core the job may use ("cpu_baseline").
 
 Prints exactly one JSON line on rank 0 (stdout); progress goes to stderr.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import importlib.util
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,16 +45,41 @@ PKG_DIR = os.environ.get("TSA_PKG_DIR", os.path.join(ROOT, "hw-accelerator-three
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 BYTES_PER_CELL = 28            # 7 int16 states written + read once
-# VALU issue ceiling: 256 CU x 4 SIMD, one wave64 VALU instruction per 4 cycles
-# per SIMD (MI355X_MICROARCH.md "vector-instruction ISSUE cost"), 2.4 GHz
+# VALU issue ceiling of the packed-16-bit wave64 instructions the pencil kernel
+# issues: 256 CU x 4 SIMD x 2.4 GHz / 4 cycles per instruction per SIMD. The
+# 4 cycles are measured (tools/valu_peak.hip -> profiles/r1_valu_peak.jsonl:
+# <= 0.24 instr/cycle/SIMD for v_pk_maximum3_f16, v_pk_add_f16, v_bfi_b32, DPP
+# movs at 1-8 waves per SIMD), not the 2-cycle issue of a 32-wide op.
 VALU_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 4
+VALU_PEAK_SOURCE = "profiles/r1_valu_peak.jsonl (tools/valu_peak.hip)"
+# Paper Table III (pic/Result.png): ASIC runtime per N^3 cube, ms
+ASIC_MS = {64: 0.03, 128: 0.19, 256: 1.39, 512: 10.82}
+
+# Kernel sources whose instruction stream a committed PMC profile describes
+# (bench refuses a profile whose stamp differs: the counters would be stale).
+KERNEL_SOURCES = {
+    "pencil_kernel": ["pencil_kernel.hip", "pencil_kernel.h", "pencil_common.h", "tsa_internal.h"],
+    "plane_step_kernel": ["plane_kernel.hip", "tsa_internal.h"],
+}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def kernel_source_hash(kernel_name: str) -> str:
+    h = hashlib.sha256()
+    for fn in KERNEL_SOURCES.get(kernel_name, []):
+        p = os.path.join(PKG_DIR, "csrc", fn)
+        if os.path.exists(p):
+            with open(p, "rb") as f:
+                h.update(fn.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def load_pkg():
+    if "tsa_amd" in sys.modules:
+        return sys.modules["tsa_amd"]
     spec = importlib.util.spec_from_file_location(
         "tsa_amd", os.path.join(PKG_DIR, "__init__.py"), submodule_search_locations=[PKG_DIR])
     mod = importlib.util.module_from_spec(spec)
@@ -56,18 +91,66 @@ def load_pkg():
 def load_pmc(kernel_name: str, workload: str) -> dict:
     """Per-launch PMC figures from the committed profile (profiles/pmc_*.json,
     written by tools/pmc_traffic.py per the MI355X_MICROARCH.md HBM recipe):
-    hbm_bytes_per_launch (FETCH_SIZE x2 + WRITE_SIZE) and valu_insts_per_launch."""
+    hbm_bytes_per_launch (2 x FETCH_SIZE + WRITE_SIZE) and
+    valu_insts_per_launch (SQ_INSTS_VALU). Refused ({"stale": ...}) when its
+    source stamp is not the hash of the kernel sources in this tree."""
     path = os.path.join(ROOT, "profiles", f"pmc_{kernel_name}_{workload}.json")
     if not os.path.exists(path):
         return {}
     try:
         with open(path) as f:
-            return json.load(f)
+            pmc = json.load(f)
     except Exception:  # noqa: BLE001
         return {}
+    want = kernel_source_hash(kernel_name)
+    if pmc.get("kernel_source_sha256") != want:
+        return {"stale": f"{os.path.relpath(path, ROOT)} stamped "
+                         f"{pmc.get('kernel_source_sha256')}, sources {want}"}
+    return pmc
 
 
-def main():
+def host_cores() -> int:
+    """Host cores this job may use: the affinity mask, capped by a cgroup CPU
+    quota (the GPU box gives each job a share of a larger machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            quota, period = open(path).read().split()[:2]
+            if quota != "max":
+                n = min(n, max(1, int(int(quota) // int(period))))
+        except (OSError, ValueError):
+            pass
+    return max(1, n)
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv: list[str], script: str = __file__) -> int:
+    """Start n rank processes of `script argv` (one per GPU) with the
+    torch.distributed env set before any of them touches a device; wait for
+    all; return the worst exit status. This process never initialises the
+    GPU (no exec either: the ranks are children)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + argv, env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return (abs(bad[0]) or 1) if bad else 0
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -78,27 +161,74 @@ def main():
     ap.add_argument("--length", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra-configs", action="store_true",
-                    help="skip the configs[1]/configs[3] single-cube timings")
+                    help="skip the single-cube timings other than configs[2]")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target wall time of the CPU-baseline sample")
     ap.add_argument("--check", type=int, default=4, help="triples checked vs the oracle")
     ap.add_argument("--score-bits", type=int, default=12,
                     help="12 = RTL wrap (default); 16/0 for cubes beyond the RTL envelope (1024^3)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+class GpuBatch:
+    """The hot path on this rank's GPU: tsa_score_batch_async over a batch
+    resident in HBM, launched on torch's current stream."""
+
+    def __init__(self, tsa, dev, seqs, offs, n, L, params, kernel):
+        import torch
+        self.torch, self.tsa = torch, tsa
+        self.n, self.L, self.params, self.kernel = n, L, params, kernel
+        self.d_seqs = torch.from_numpy(seqs).to(dev)
+        self.d_offs = torch.from_numpy(offs).to(dev)
+        self.d_scores = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+        self.ws = tsa.workspace_size(max(n, 1), L, L, L, params, kernel)
+        self.d_ws = torch.empty(max(self.ws, 16), dtype=torch.uint8, device=dev)
+        self.stream = torch.cuda.current_stream()
+        self.ev = None
+
+    def step(self):
+        if self.n:
+            self.tsa.score_batch_async(self.d_seqs.data_ptr(), self.d_offs.data_ptr(), self.n,
+                                       self.L, self.L, self.L, self.d_scores.data_ptr(),
+                                       self.d_ws.data_ptr(), self.ws, self.stream.cuda_stream,
+                                       self.params, self.kernel)
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def mark(self):  # HIP events on the launch stream (torch events see only torch's stream)
+        e = self.torch.cuda.Event(enable_timing=True)
+        e.record(self.stream)
+        return e
+
+    @staticmethod
+    def elapsed_ms(e0, e1):
+        return e0.elapsed_time(e1)
+
+    def scores(self):
+        return self.d_scores[: self.n]
+
+
+def run_rank(args, world: int, rank: int, local_rank: int, backend: str, make_batch,
+             device=None, extras: bool = True, on_scores=None):
+    """One rank of the bench: shard, stage, warm up, time K steps between
+    barriers, take the max over ranks, gather the scores (the one collective)
+    and, on rank 0, return the JSON record. make_batch(tsa, dev, seqs, offs, n,
+    L, params, kernel) builds the rank's scorer (GpuBatch on the box)."""
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+        assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
+    elif backend == "nccl":
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
 
     tsa = load_pkg()
     import tsa_amd.synth as synth  # noqa: E402
@@ -114,36 +244,25 @@ def main():
     # ---- inputs resident in HBM before timing --------------------------------
     seqs, offs = synth.batch(i0, n, L)
     offs = offs - offs[0]
-    d_seqs = torch.from_numpy(seqs).to(dev)
-    d_offs = torch.from_numpy(offs).to(dev)
-    d_scores = torch.zeros(n, dtype=torch.int32, device=dev)
-    ws_bytes = tsa.workspace_size(n, L, L, L, params, args.kernel)
-    d_ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream()
-
-    def step():
-        tsa.score_batch_async(d_seqs.data_ptr(), d_offs.data_ptr(), n, L, L, L,
-                              d_scores.data_ptr(), d_ws.data_ptr(), ws_bytes, stream.cuda_stream,
-                              params, args.kernel)
+    hot = make_batch(tsa, dev, seqs, offs, n, L, params, args.kernel)
 
     for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+        hot.step()
+    hot.sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    hot.sync()
     t0 = time.perf_counter()
-    ev0.record(stream)
+    ev0 = hot.mark()
     for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
+        hot.step()
+    ev1 = hot.mark()
+    hot.sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    hot.sync()
     elapsed = time.perf_counter() - t0
-    kernel_ms_per_step = ev0.elapsed_time(ev1) / args.steps
+    kernel_ms_per_step = hot.elapsed_ms(ev0, ev1) / args.steps
     elapsed_max = shard.max_over_ranks(elapsed, dev)
 
     cells_per_triple = L * L * L
@@ -151,120 +270,75 @@ def main():
     gcups = total_cells / elapsed_max / 1e9
     ms_per_step = elapsed_max / args.steps * 1e3
 
-    # ---- score gather (the one collective) + parity sample --------------------
-    all_scores = shard.gather_scores(d_scores, n_total, world).cpu().numpy()
+    # ---- score gather (the one collective) ------------------------------------
+    all_scores = shard.gather_scores(hot.scores(), n_total, world).cpu().numpy()
 
-    if rank != 0:
-        if world > 1:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
+    rec = None
+    if rank == 0:
+        rec = report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gcups,
+                     ms_per_step, kernel_ms_per_step, all_scores, extras)
+        if on_scores is not None:  # test hook: the gathered scores, global order
+            on_scores(rec, all_scores)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return rec
 
+
+def report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gcups, ms_per_step,
+           kernel_ms_per_step, all_scores, extras):
     kind = args.kernel
     if kind == "auto":  # AUTO = pencil whenever its factored arithmetic is exact
         kind = "pencil" if _pencil_ok(tsa, L, params) else "plane"
     kernel_name = {"plane": "plane_step_kernel", "pencil": "pencil_kernel"}[kind]
     launches_per_step = (3 * L - 1) if kind == "plane" else 1
     # kernel, arithmetic and schedule the library picks (host-only query)
-    plan = tsa.describe_plan(per_gpu, L, L, L, params, kernel=kind, sync=False)
+    plan = tsa.describe_plan(max(per_gpu, 1), L, L, L, params, kernel=kind, sync=False)
     # exact integer values in f16 / int16 lanes; plane: int32 math on int16 planes
     arith = "f16" if " f16 " in plan else ("i32" if plan == "plane" else "i16")
 
-    # per-rank kernel time of THIS rank's stream (HIP events on the launch stream)
-    per_gpu_cells = n * cells_per_triple
-    achieved_gbs = per_gpu_cells * BYTES_PER_CELL / (kernel_ms_per_step * 1e-3) / 1e9
+    per_gpu_cells = n * L * L * L
+    kernel_s = kernel_ms_per_step * 1e-3
+    algo_gbs = per_gpu_cells * BYTES_PER_CELL / kernel_s / 1e9
     pmc = load_pmc(kernel_name, args.workload) if (L == 256 and per_gpu == 512) else {}
+    if pmc.get("stale"):
+        log("PMC profile refused:", pmc["stale"])
     traffic = pmc.get("hbm_bytes_per_launch")
-    valu = None
-    if pmc.get("valu_insts_per_launch") and kind == "pencil":
-        # the binding resource of the pencil kernel: VALU issue (states never
-        # leave the chip, so the 28 B/cell streaming roofline is exceeded)
-        insts = pmc["valu_insts_per_launch"]
-        ach = insts / (kernel_ms_per_step * 1e-3)
-        valu = {"bound": "valu", "achieved": round(ach / 1e9, 2), "peak": VALU_WAVE_INSTR_PER_S / 1e9,
-                "unit": "G wave-instr/s", "frac": round(ach / VALU_WAVE_INSTR_PER_S, 4),
-                "insts_per_launch": insts,
-                "lane_insts_per_cell": round(insts * 64 / per_gpu_cells, 3),
-                "source": f"SQ_INSTS_VALU, profiles/pmc_{kernel_name}_{args.workload}.json"}
+    insts = pmc.get("valu_insts_per_launch")
+    hbm = {"bound": "hbm", "achieved": round(traffic / kernel_s / 1e9, 2) if traffic else None,
+           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(traffic / kernel_s / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+           "bytes_per_launch": traffic,
+           "bytes_per_cell": round(traffic / per_gpu_cells, 3) if traffic else None,
+           "source": "2 x FETCH_SIZE + WRITE_SIZE (rocprofv3 --pmc, separate passes; gfx950 "
+                     f"FETCH_SIZE correction), profiles/pmc_{kernel_name}_{args.workload}.json"}
+    hbm_model = {"bound": "hbm", "bytes_per_cell": BYTES_PER_CELL, "achieved": round(algo_gbs, 2),
+                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(algo_gbs / HBM_PEAK_GBS, 4),
+                 "note": "SURVEY.md 8d: 7 int16 states written + read once per cell; the pencil "
+                         "kernel keeps states in registers/LDS, so this model is not its ceiling"}
+    if insts and kind == "pencil":
+        # the binding resource of the pencil kernel: VALU issue
+        ach = insts / kernel_s
+        roofline = {"bound": "valu", "achieved": round(ach / 1e9, 2),
+                    "peak": VALU_WAVE_INSTR_PER_S / 1e9, "unit": "G wave-instr/s",
+                    "frac": round(ach / VALU_WAVE_INSTR_PER_S, 4), "traffic": traffic,
+                    "peak_source": VALU_PEAK_SOURCE, "insts_per_launch": insts,
+                    "lane_insts_per_cell": round(insts * 64 / per_gpu_cells, 3),
+                    "source": f"SQ_INSTS_VALU per launch (profiles/pmc_{kernel_name}_"
+                              f"{args.workload}.json) / live kernel time (HIP events)"}
+    else:  # no current profile: the contract's HBM form on algorithmic bytes
+        roofline = dict(hbm_model, traffic=traffic)
+    roofline.update({"kernel": kernel_name, "kernel_ms_per_step": round(kernel_ms_per_step, 4),
+                     "hbm": hbm, "hbm_model": hbm_model, "pmc_stale": pmc.get("stale")})
 
-    # single-cube latency: configs[2] (L^3, params as the batch), plus configs[1]
-    # (64^3) and configs[3] (1024^3, 16-bit words: beyond the RTL envelope)
-    def time_single(Ls, prm, reps=5):
-        sa = synth.batch(0, 1, Ls)
-        s_seqs = torch.from_numpy(sa[0]).to(dev)
-        s_offs = torch.from_numpy(sa[1]).to(dev)
-        s_score = torch.zeros(1, dtype=torch.int32, device=dev)
-        s_ws = tsa.workspace_size(1, Ls, Ls, Ls, prm, args.kernel)
-        s_wsb = torch.empty(max(s_ws, 16), dtype=torch.uint8, device=dev)
+    single = {}
+    if extras:
+        single = time_singles(args, tsa, synth, hot, dev, L, params)
+    parity, cpu_baseline = None, None
+    if extras and args.check > 0:
+        parity, cpu_baseline = oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single)
 
-        def sstep():
-            tsa.score_batch_async(s_seqs.data_ptr(), s_offs.data_ptr(), 1, Ls, Ls, Ls,
-                                  s_score.data_ptr(), s_wsb.data_ptr(), s_ws, stream.cuda_stream,
-                                  prm, args.kernel)
-        sstep()
-        torch.cuda.synchronize()
-        times = []  # median of individually timed calls (a latency, not a throughput)
-        for _ in range(reps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            sstep()
-            e1.record(stream)
-            torch.cuda.synchronize()
-            times.append(e0.elapsed_time(e1))
-        sms = float(np.median(times))
-        return {"ms": round(sms, 4), "gcups": round(Ls ** 3 / (sms * 1e-3) / 1e9, 3),
-                "score": int(s_score.item()), "score_bits": prm.score_bits}
-
-    single = None
-    other_configs = {}
-    try:
-        single = {"config": f"configs[2]: one {L}^3 triple", **time_single(L, params)}
-        if not args.no_extra_configs:
-            other_configs["configs[1]: one 64^3 triple"] = time_single(64, params, reps=10)
-            other_configs["configs[3]: one 1024^3 triple"] = time_single(
-                1024, tsa.TsaParams.default(score_bits=16), reps=7)
-    except Exception as e:  # noqa: BLE001
-        log("single-cube measurement failed:", e)
-
-    # parity sample vs the CPU oracle (checker only)
-    parity = None
-    cpu_baseline = None
-    try:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle  # noqa: E402
-        nthreads = max(1, min(16, os.cpu_count() or 1))
-        idx = sorted(set([0, n_total - 1] + [int(v) for v in np.linspace(0, n_total - 1, args.check)]))
-        trip = [synth.triple(i, L) for i in idx]
-        cs, co = tsa.pack_batch(trip)
-        oparams = oracle.default_params(score_bits=args.score_bits)
-        ref = oracle.score_batch(cs, co, oparams, nthreads=nthreads)
-        got = all_scores[idx]
-        parity = {"checked": len(idx), "mismatches": int((ref != got).sum()),
-                  "against": "oracle/tsa_oracle.c"}
-        if single is not None:
-            parity["single_cube_ok"] = bool(single["score"] == int(ref[0]))
-        if world == 1 and not args.no_cpu_baseline:
-            # bounded sample of the same workload: one 256^3 triple per thread per round
-            t_one = oracle.now()
-            oracle.score_batch(cs[: 3 * L], co[:4], oparams, nthreads=1)
-            t_one = oracle.now() - t_one
-            rounds = max(1, int(args.cpu_seconds / max(t_one, 1e-3)))
-            ns = nthreads * rounds
-            bs, bo = synth.batch(0, ns, L)
-            t = oracle.now()
-            oracle.score_batch(bs, bo, oparams, nthreads=nthreads)
-            t = oracle.now() - t
-            cpu_baseline = {
-                "value": round(ns * cells_per_triple / t / 1e9, 5), "unit": "GCUPS",
-                "cores": nthreads, "kind": "port",
-                "sample": f"{ns} synthetic {L}^3 triples (same generator) on {nthreads} threads, "
-                          f"{t:.1f} s wall; 1-thread rate {cells_per_triple / t_one / 1e9:.4f} GCUPS; "
-                          f"oracle/tsa_oracle.c literal RTL form, gcc -O2",
-            }
-    except Exception as e:  # noqa: BLE001
-        log("oracle leg failed:", e)
-
-    out = {
+    return {
         "metric": "GCUPS (10^9 3D-DP cell updates/s), 256^3 cubes",
         "value": round(gcups, 3),
         "unit": "GCUPS",
@@ -278,29 +352,118 @@ def main():
         "dtype": arith,
         "data": "synthetic (splitmix64 uniform DNA, SURVEY.md 8d seeds)",
         "config": {
-            "workload": (f"batch: {per_gpu} independent {L}^3 triples per GPU (configs[4] per-GPU shard)"
-                         if args.workload == "batch" else f"single: one {L}^3 triple per GPU (configs[2])"),
+            "workload": (f"batch: {per_gpu} independent {L}^3 triples per GPU -- the per-GPU shard "
+                         f"of configs[4] (4096 x 256^3 over 8 GPUs); value = all ranks' cells / "
+                         f"max-over-ranks time" if args.workload == "batch"
+                         else f"single: one {L}^3 triple per GPU (configs[2])"),
+            "config_index": 4 if args.workload == "batch" else 2,
             "length": L, "triples_per_gpu": per_gpu, "triples_total": n_total,
             "kernel": kind, "plan": plan, "launches_per_step": launches_per_step,
-            "parallelism": f"shard{world}", "score_bits": params.score_bits,
+            "parallelism": f"shard{world}", "world_size": world, "score_bits": params.score_bits,
         },
-        "roofline": {
-            "bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
-            "kernel": kernel_name, "bytes_per_cell": BYTES_PER_CELL,
-            "kernel_ms_per_step": round(kernel_ms_per_step, 4),
-            "traffic_bytes_per_cell": (round(traffic / per_gpu_cells, 3) if traffic else None),
-            "valu": valu,
-        },
+        "roofline": roofline,
         "cpu_baseline": cpu_baseline,
         "single_cube": single,
-        "other_configs": other_configs,
         "parity": parity,
     }
-    print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+
+
+def time_singles(args, tsa, synth, hot, dev, L, params):
+    """Single-cube latency: configs[2] (L^3, params as the batch), configs[1]
+    (64^3), the paper's 128^3 and 512^3 (Table III, RTL 12-bit words) and
+    configs[3] (1024^3, 16-bit words: beyond the RTL envelope). Median of
+    individually timed calls on the launch stream (a latency)."""
+    import torch
+    stream = hot.stream
+
+    def one(Ls, prm, reps):
+        sa = synth.batch(0, 1, Ls)
+        s_seqs = torch.from_numpy(sa[0]).to(dev)
+        s_offs = torch.from_numpy(sa[1]).to(dev)
+        s_score = torch.zeros(1, dtype=torch.int32, device=dev)
+        s_ws = tsa.workspace_size(1, Ls, Ls, Ls, prm, args.kernel)
+        s_wsb = torch.empty(max(s_ws, 16), dtype=torch.uint8, device=dev)
+
+        def sstep():
+            tsa.score_batch_async(s_seqs.data_ptr(), s_offs.data_ptr(), 1, Ls, Ls, Ls,
+                                  s_score.data_ptr(), s_wsb.data_ptr(), s_ws, stream.cuda_stream,
+                                  prm, args.kernel)
+        sstep()
+        torch.cuda.synchronize()
+        times = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            sstep()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1))
+        sms = float(np.median(times))
+        r = {"ms": round(sms, 4), "gcups": round(Ls ** 3 / (sms * 1e-3) / 1e9, 3),
+             "score": int(s_score.item()), "score_bits": prm.score_bits,
+             "plan": tsa.describe_plan(1, Ls, Ls, Ls, prm, kernel=args.kernel, sync=False)}
+        if Ls in ASIC_MS and prm.score_bits == 12:
+            r["asic_ms"] = ASIC_MS[Ls]
+            r["vs_asic"] = round(ASIC_MS[Ls] / sms, 3)
+        return r
+
+    out = {}
+    try:
+        out[f"configs[2]: {L}^3"] = one(L, params, 7)
+        if not args.no_extra_configs:
+            out["configs[1]: 64^3"] = one(64, params, 15)
+            out["paper N=128: 128^3"] = one(128, params, 9)
+            out["paper N=512: 512^3"] = one(512, params, 5)
+            out["configs[3]: 1024^3 (16-bit words)"] = one(
+                1024, tsa.TsaParams.default(score_bits=16), 5)
+    except Exception as e:  # noqa: BLE001
+        log("single-cube measurement failed:", e)
+    return out
+
+
+def oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single):
+    """Checker + CPU baseline (the only use of oracle/ here): a sample of the
+    gathered scores vs the C oracle, and at N=1 the oracle timed on a bounded
+    sample of the same workload on every host core the job may use."""
+    parity, cpu_baseline = None, None
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # noqa: E402
+        cores = host_cores()
+        idx = sorted(set([0, n_total - 1] + [int(v) for v in np.linspace(0, n_total - 1, args.check)]))
+        trip = [synth.triple(i, L) for i in idx]
+        cs, co = tsa.pack_batch(trip)
+        oparams = oracle.default_params(score_bits=args.score_bits)
+        ref = oracle.score_batch(cs, co, oparams, nthreads=cores)
+        got = all_scores[idx]
+        parity = {"checked": len(idx), "mismatches": int((ref != got).sum()),
+                  "against": "oracle/tsa_oracle.c"}
+        key = f"configs[2]: {L}^3"
+        if key in single:
+            parity["single_cube_ok"] = bool(single[key]["score"] == int(ref[0]))
+        if world == 1 and not args.no_cpu_baseline:
+            # bounded sample of the same workload: one L^3 triple per thread per round
+            t_one = oracle.now()
+            oracle.score_batch(cs[: 3 * L], co[:4], oparams, nthreads=1)
+            t_one = oracle.now() - t_one
+            rounds = max(1, int(args.cpu_seconds / max(t_one, 1e-3)))
+            ns = cores * rounds
+            bs, bo = synth.batch(0, ns, L)
+            t = oracle.now()
+            oracle.score_batch(bs, bo, oparams, nthreads=cores)
+            t = oracle.now() - t
+            cpu_baseline = {
+                "value": round(ns * L ** 3 / t / 1e9, 5), "unit": "GCUPS",
+                "cores": cores, "kind": "port",
+                "sample": f"{ns} synthetic {L}^3 triples (same generator) on {cores} threads "
+                          f"(all host cores this job may use: affinity mask / cgroup quota; "
+                          f"os.cpu_count()={os.cpu_count()}), {t:.1f} s wall; 1-thread rate "
+                          f"{L ** 3 / t_one / 1e9:.4f} GCUPS; oracle/tsa_oracle.c literal RTL "
+                          f"form, gcc -O2",
+            }
+    except Exception as e:  # noqa: BLE001
+        log("oracle leg failed:", e)
+    return parity, cpu_baseline
 
 
 def _pencil_ok(tsa, L, params):
@@ -309,6 +472,22 @@ def _pencil_ok(tsa, L, params):
         return True
     except tsa.TsaError:
         return False
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # started directly: become the launcher of args.gpus rank processes
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:] if argv is None else list(argv)))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    rec = run_rank(args, world, rank, local_rank, "nccl", GpuBatch)
+    if rec is not None:
+        print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

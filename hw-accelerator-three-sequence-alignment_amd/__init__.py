@@ -60,7 +60,11 @@ EXPORTS = (
     "tsa_default_params", "tsa_validate", "tsa_score_gpu", "tsa_score_gpu_ex",
     "tsa_score_batch", "tsa_batch_workspace_size", "tsa_score_batch_async",
     "tsa_device_count", "tsa_strerror", "tsa_version", "tsa_describe_plan", "tsa_align_gpu",
+    "tsa_fallback_count",
 )
+
+# Score of a triple the device could not score (include/trialign.h).
+SCORE_INVALID = -(2 ** 31)
 
 # Alignment columns (tsa_align_gpu): the state of each column and which of
 # (A, B, C) it consumes -- the predecessor offsets of src/PE_1cyc.v:164-218.
@@ -128,6 +132,8 @@ def _load_lib() -> ctypes.CDLL:
                                                             ctypes.c_char_p, ctypes.c_size_t]
     lib.tsa_align_gpu.argtypes = [u8p, ctypes.c_int32, u8p, ctypes.c_int32, u8p, ctypes.c_int32,
                                   pp, i32p, u8p, ctypes.c_int32, i32p, i32p, ctypes.c_int32]
+    lib.tsa_fallback_count.argtypes = []
+    lib.tsa_fallback_count.restype = ctypes.c_int64
     lib.tsa_device_count.argtypes = []
     lib.tsa_strerror.argtypes = [ctypes.c_int]
     lib.tsa_strerror.restype = ctypes.c_char_p
@@ -154,6 +160,12 @@ def version() -> str:
 
 def device_count() -> int:
     return int(_lib.tsa_device_count())
+
+
+def fallback_count() -> int:
+    """Lap hand-offs that timed out on the synchronous paths so far (each was
+    rescored by the helix kernel); 0 in a healthy run."""
+    return int(_lib.tsa_fallback_count())
 
 
 def _as_u8(seq) -> np.ndarray:
@@ -357,12 +369,118 @@ def score_batch_async(d_seqs_ptr: int, d_offsets_ptr: int, n: int, max_la: int, 
     _check(rc, "tsa_score_batch_async")
 
 
-def read_sequence(path: str) -> np.ndarray:
-    """dat (one decimal symbol per line, CRLF tolerant -- dat/A_seq.dat) or
-    FASTA (A=0 T=1 C=2 G=3 N=4, src/TriAlign_tb.sv:42-46)."""
+# ---- the testbench's sequence RAM image (src/TriAlign_tb.sv:94-96,149-169) ----
+# ``reg [127:0] seqX_ram [...]``: 32 four-bit symbols per 128-bit word, symbol
+# i in word i >> 5 at bits [4*(i & 31) + 3 : 4*(i & 31)] (the read mux of
+# src/TriAlign_tb.sv:149-169). As little-endian bytes that is two symbols per
+# byte, the even one in the low nibble.
+RAM_WORD_SYMBOLS = 32
+
+
+def pack_ram128(seq) -> np.ndarray:
+    """Symbols -> the testbench RAM image, as an (n_words, 16) uint8 array of
+    little-endian 128-bit words (unused nibbles zero)."""
+    s = _as_u8(seq)
+    if s.size and int(s.max()) > 15:
+        raise TsaError(TSA_EINVAL, "symbol does not fit a 4-bit RAM nibble")
+    nw = max(1, -(-len(s) // RAM_WORD_SYMBOLS))
+    nib = np.zeros(nw * RAM_WORD_SYMBOLS, np.uint8)
+    nib[: len(s)] = s
+    return (nib[0::2] | (nib[1::2] << 4)).reshape(nw, 16)
+
+
+def unpack_ram128(words, length: int) -> np.ndarray:
+    """The first ``length`` symbols of a testbench RAM image ((n, 16) uint8
+    little-endian words, or raw bytes)."""
+    b = np.ascontiguousarray(np.asarray(words, dtype=np.uint8)).reshape(-1)
+    if length < 0 or length > 2 * b.size:
+        raise TsaError(TSA_EINVAL, "RAM image shorter than the sequence")
+    nib = np.empty(2 * b.size, np.uint8)
+    nib[0::2] = b & 15
+    nib[1::2] = b >> 4
+    return nib[:length].copy()
+
+
+def ram128_hex_lines(seq) -> list[str]:
+    """The RAM image as ``$readmemh`` lines: one 128-bit word per line, 32 hex
+    digits, most significant nibble (symbol 31 of the word) first."""
+    return ["".join(f"{v:x}" for v in unpack_ram128(w, 32)[::-1]) for w in pack_ram128(seq)]
+
+
+def _parse_ram_hex(text: str, length: Optional[int]) -> np.ndarray:
+    words = []
+    for ln in text.splitlines():
+        ln = ln.split("//")[0].strip().replace("_", "")
+        if not ln or ln.startswith("@"):
+            continue
+        if len(ln) > 32 or any(ch not in "0123456789abcdefABCDEF" for ch in ln):
+            raise TsaError(TSA_EINVAL, f"RAM word {ln!r}")
+        nibs = [int(ch, 16) for ch in ln.rjust(32, "0")][::-1]  # symbol 0 = lowest nibble
+        words.extend(nibs)
+    seq = np.asarray(words, dtype=np.uint8)
+    return seq if length is None else seq[:length]
+
+
+_TB_INIT = None
+
+
+def _parse_tb_initial(text: str, name: str) -> np.ndarray:
+    """Symbols a testbench ``initial`` block writes into ``name``: lines
+    ``seqA_ram[w][hi:lo] <= A;`` (src/TriAlign_tb.sv:423-1960), symbol index
+    32*w + lo/4, names A/T/C/G/N or numbers (src/TriAlign_tb.sv:42-46)."""
+    import re
+    global _TB_INIT
+    if _TB_INIT is None:
+        _TB_INIT = re.compile(r"(\w+)\[(\d+)\]\[(\d+):(\d+)\]\s*<?=\s*(?:4'[dhb])?(\w+)\s*;")
+    got = {}
+    for m in _TB_INIT.finditer(text):
+        if m.group(1) != name:
+            continue
+        w, hi, lo, v = int(m.group(2)), int(m.group(3)), int(m.group(4)), m.group(5)
+        if hi - lo != 3 or lo % 4 or hi >= 128:
+            raise TsaError(TSA_EINVAL, f"RAM nibble [{hi}:{lo}]")
+        sym = SYMBOLS[v] if v in SYMBOLS else int(v, 0)
+        if sym > 4:
+            raise TsaError(TSA_EINVAL, f"symbol {v}")
+        got[32 * w + lo // 4] = sym
+    if not got:
+        raise TsaError(TSA_EINVAL, f"no {name} writes found")
+    n = max(got) + 1
+    if sorted(got) != list(range(n)):
+        raise TsaError(TSA_EINVAL, f"{name}: symbols missing")
+    return np.asarray([got[i] for i in range(n)], dtype=np.uint8)
+
+
+def read_sequence(path: str, fmt: str = "auto", length: Optional[int] = None,
+                  ram: str = "seqA_ram") -> np.ndarray:
+    """Read one sequence. Formats (``fmt``):
+
+    * ``dat`` -- one decimal symbol per line, CRLF tolerant (dat/A_seq.dat);
+    * ``fasta`` -- A=0 T=1 C=2 G=3 N=4 (src/TriAlign_tb.sv:42-46);
+    * ``ramhex`` -- the testbench's 128-bit sequence RAM as ``$readmemh`` text,
+      32 symbols per word (src/TriAlign_tb.sv:94-96,149-169); ``length``
+      trims the padding of the last word;
+    * ``ramraw`` -- the same RAM image as raw little-endian 16-byte words
+      (``length`` required);
+    * ``tb`` -- the ``seqX_ram[w][hi:lo] <= SYM;`` writes of a testbench
+      ``initial`` block (src/TriAlign_tb.sv:423-1960), RAM named by ``ram``.
+
+    ``auto`` tells FASTA (``>``), testbench initial blocks (``<=``) and dat
+    apart; RAM images need an explicit ``fmt``."""
+    if fmt == "ramraw":
+        if length is None:
+            raise TsaError(TSA_EINVAL, "ramraw needs the sequence length")
+        return unpack_ram128(np.fromfile(path, dtype=np.uint8), length)
     with open(path, "r") as f:
         text = f.read()
+    if fmt == "ramhex":
+        return _parse_ram_hex(text, length)
     body = text.lstrip()
+    if fmt == "tb" or (fmt == "auto" and "<=" in body and "_ram[" in body):
+        seq = _parse_tb_initial(body, ram)
+        return seq if length is None else seq[:length]
+    if fmt not in ("auto", "dat", "fasta"):
+        raise TsaError(TSA_EINVAL, f"format {fmt!r}")
     if body.startswith(">"):
         lines = body.splitlines()[1:]
         seq = []

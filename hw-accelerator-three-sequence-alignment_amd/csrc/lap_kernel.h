@@ -1,0 +1,40 @@
+// lap_kernel.h -- host interface of the single-cube (lap) schedule
+// (lap_kernel.hip), used by the pencil dispatcher (pencil_kernel.hip).
+#pragma once
+
+#include "pencil_kernel.h"
+
+namespace tsa {
+
+struct PencilArgs;
+
+struct LapGeom {
+  int32_t M, NW;     // packed pairs per lane (tile = 64 M positions), waves (2 NW rows)
+  int32_t G, GZ;     // laps, z-tiles
+  int32_t NC, CH;    // columns (triple, z-tile) and columns per XCD (blocks = G * CH * 8)
+  int32_t YR, ZR;    // y / z ring slots per workgroup (powers of 2)
+  int32_t per_cu;    // workgroups a CU holds (occupancy API on the kernel)
+  int64_t blocks;    // grid (padding blocks for the XCD-aware tile mapping)
+  size_t lds, prog_bytes, yf_bytes, zf_bytes;
+  int64_t waves;     // dispatch waves: 1 = every workgroup resident at once
+  double est_us;     // estimated latency
+  bool ok;           // feasible and more than one workgroup per triple
+};
+
+// A grid beyond the resident slots runs in dispatch waves; streaming is
+// limited to a few of them.
+constexpr int64_t LAP_MAX_WAVES = 3;
+
+// Geometry of the lap schedule (M pairs per lane, NW waves) for a batch of n
+// triples; full_rings: rings as long as the cube (no back-pressure -- the form a
+// grid beyond the resident slots needs).
+LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW,
+                 bool full_rings, bool f16, bool sop);
+size_t lap_workspace_bytes(const LapGeom &g);
+// Launch it. d_err (synchronous callers): the error word, cleared before the
+// launch, nonzero after it when a hand-off timed out.
+int lap_launch(const LapGeom &g, bool f16, bool sop, const uint8_t *d_seqs,
+               const int64_t *d_offsets, int32_t n, int32_t *d_scores, void *d_ws,
+               const PencilArgs &pa, hipStream_t stream, int32_t **d_err);
+
+}  // namespace tsa

@@ -5,23 +5,32 @@
 
 namespace tsa {
 
-// Headroom (score units) the pencil kernel's int16 lanes keep beyond the
-// a-priori value bound: message biases and penalties are applied in int16.
-constexpr int64_t PENCIL_MARGIN = 512;
+// Headroom (score units) the factored form needs beyond the a-priori bound on
+// candidates and states (value_bound): its messages max_s(S[s] - P[T][s]) sit
+// one score below a candidate, the f16 form folds the mismatch into them and
+// adds the triple score in two parts. Every such intermediate lies within
+// [lo - slack, hi + slack], so the carrier (int16, or exact
+// f16 integers in [-2048, 2048]) must hold that interval.
+int64_t pencil_slack(int32_t match, int32_t mismatch, int32_t gap_open, int32_t gap_extend);
 
 bool pencil_supported(const tsa_params *p);
 bool pencil_shape_supported(int32_t max_la, int32_t max_lb, int32_t max_lc);
-// stream_ok: the lap kernel may use a grid larger than the resident slots (needs
-// in-order block dispatch; the caller must check *d_err after the launch and
-// rerun with stream_ok = false if it is set)
+// Which single-cube (lap) schedules a launch may use:
+//   LAP_OFF      -- helix only (no cross-workgroup dependency at all);
+//   LAP_RESIDENT -- the lap kernel when its whole grid is co-resident;
+//   LAP_STREAM   -- also grids beyond the resident slots (relies on in-order
+//                   block dispatch; the caller must check *d_err after the
+//                   launch and rescore with LAP_OFF when it is set).
+// A lap launch that times out reports TSA_SCORE_INVALID for its triples.
+enum LapPolicy { LAP_OFF = 0, LAP_RESIDENT = 1, LAP_STREAM = 2 };
 size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
-                              bool stream_ok);
+                              const KParams &kp, const Range &bound, LapPolicy lap);
 // The plan pencil_launch_batch would run, as text (tsa_describe_plan).
 void pencil_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
-                     const Range &bound, bool stream_ok, char *buf, size_t len);
+                     const Range &bound, LapPolicy lap, char *buf, size_t len);
 int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                         int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
                         const Range &bound, int32_t *d_scores, void *d_ws, size_t ws_bytes,
-                        hipStream_t stream, bool stream_ok, int32_t **d_err);
+                        hipStream_t stream, LapPolicy lap, int32_t **d_err);
 
 }  // namespace tsa

@@ -166,14 +166,20 @@ int tsa_validate(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb, con
 namespace tsa {
 
 // Is the factored (pencil) arithmetic bit-identical to the literal RTL form
-// for every triple of these lengths? True when no candidate can wrap at
-// score_bits and everything fits the pencil kernel's int16 lanes.
+// for every triple of these lengths? Two separate conditions:
+//  (1) no candidate can wrap at score_bits -- the bare bound, which already
+//      covers every candidate and state (value_bound), against the RTL word;
+//  (2) the kernel's carrier holds every intermediate of the factored form:
+//      the bound widened by pencil_slack inside int16 (use_f16 applies the
+//      same test against the exact-f16 range to pick the f16 arithmetic).
 static bool pencil_exact(const tsa_params *p, int64_t la, int64_t lb, int64_t lc) {
   const Range r = value_bound(p, la, lb, lc);
-  const int64_t lim_lo = p->score_bits ? -(1LL << (p->score_bits - 1)) : -32768;
-  const int64_t lim_hi = p->score_bits ? (1LL << (p->score_bits - 1)) - 1 : 32767;
-  return r.lo - PENCIL_MARGIN >= std::max<int64_t>(lim_lo, -32768) &&
-         r.hi + PENCIL_MARGIN <= std::min<int64_t>(lim_hi, 32767) && pencil_supported(p) &&
+  if (p->score_bits) {
+    const int64_t lim_lo = -(1LL << (p->score_bits - 1)), lim_hi = (1LL << (p->score_bits - 1)) - 1;
+    if (r.lo < lim_lo || r.hi > lim_hi) return false;
+  }
+  const int64_t slack = pencil_slack(p->match, p->mismatch, p->gap_open, p->gap_extend);
+  return r.lo - slack >= -32768 && r.hi + slack <= 32767 && pencil_supported(p) &&
          pencil_shape_supported((int32_t)la, (int32_t)lb, (int32_t)lc);
 }
 
@@ -184,17 +190,25 @@ static int choose_kernel(int32_t kernel, const tsa_params *p, int64_t la, int64_
   return ok ? TSA_KERNEL_PENCIL : TSA_KERNEL_PLANE;
 }
 
-// stream_ok: only the synchronous paths, which check the lap kernel's error word
+// lap: LAP_STREAM only on the synchronous paths, which check the lap kernel's
+// error word and rescore with LAP_OFF; the async path keeps LAP_RESIDENT
 static size_t workspace_for(int kind, int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
-                            bool stream_ok = false) {
+                            const tsa_params *p, LapPolicy lap = LAP_RESIDENT) {
   if (kind == TSA_KERNEL_PLANE) return plane_workspace_bytes(n, max_la, max_lb, max_lc);
-  return pencil_workspace_bytes(n, max_la, max_lb, max_lc, stream_ok);
+  KParams kp;
+  if (build_kparams(p, &kp)) return 0;
+  return pencil_workspace_bytes(n, max_la, max_lb, max_lc, kp, value_bound(p, max_la, max_lb, max_lc),
+                                lap);
 }
+
+// Lap hand-offs that timed out on the synchronous path (each rescored by the
+// helix kernel), process-wide; tsa_fallback_count() reads it.
+static std::atomic<int64_t> g_lap_fallbacks{0};
 
 static int launch_kind(int kind, const uint8_t *d_seqs, const int64_t *d_off, int32_t n,
                        int32_t max_la, int32_t max_lb, int32_t max_lc, const tsa_params *p,
                        int32_t *d_scores, int32_t *d_final7, void *ws, size_t ws_bytes,
-                       hipStream_t s, bool stream_ok = false, int32_t **d_err = nullptr) {
+                       hipStream_t s, LapPolicy lap = LAP_RESIDENT, int32_t **d_err = nullptr) {
   KParams kp;
   int rc = build_kparams(p, &kp);
   if (rc) return rc;
@@ -203,7 +217,7 @@ static int launch_kind(int kind, const uint8_t *d_seqs, const int64_t *d_off, in
                               ws, ws_bytes, s);
   return pencil_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp,
                              value_bound(p, max_la, max_lb, max_lc), d_scores, ws, ws_bytes, s,
-                             stream_ok, d_err);
+                             lap, d_err);
 }
 
 #define HIPCHK(x)                                   \
@@ -227,14 +241,18 @@ static int run_host_batch_on_device(int device, const uint8_t *seqs, const int64
   }
   const int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
   if (kind < 0) return TSA_ERANGE;
-  // chunk so the workspace stays under ~8 GiB and grid.z under 65535; the
-  // workspace is what the chunk's plan (or its fallback) needs
-  const size_t per = std::max(workspace_for(kind, 1, max_la, max_lb, max_lc, true),
-                              workspace_for(kind, 1, max_la, max_lb, max_lc, false));
-  int32_t chunk = (int32_t)std::max<size_t>(1, std::min<size_t>((size_t)8 << 30, (size_t)n * per) / per);
-  chunk = std::min(chunk, std::min(n, 65535));
-  const size_t ws_bytes = std::max(workspace_for(kind, chunk, max_la, max_lb, max_lc, true),
-                                   workspace_for(kind, chunk, max_la, max_lb, max_lc, false));
+  // chunk so the workspace stays under ~8 GiB and the grid under 65535
+  // triples; the workspace is what the chunk's own plan (lap for a few cubes,
+  // the helix ring otherwise) and its helix fallback need
+  auto ws_of = [&](int32_t c) {
+    return std::max(workspace_for(kind, c, max_la, max_lb, max_lc, p, LAP_STREAM),
+                    workspace_for(kind, c, max_la, max_lb, max_lc, p, LAP_OFF));
+  };
+  const size_t cap = (size_t)8 << 30;
+  int32_t chunk = std::min(n, 65535);
+  while (chunk > 1 && ws_of(chunk) > cap)
+    chunk = std::max<int32_t>(1, std::min<int32_t>(chunk - 1, (int32_t)((double)chunk * cap / ws_of(chunk))));
+  const size_t ws_bytes = ws_of(chunk);
   const int64_t base = offsets[3 * (int64_t)i0];
   const int64_t nbytes = offsets[3 * (int64_t)i1] - base;
   uint8_t *d_seqs = nullptr;
@@ -262,14 +280,22 @@ static int run_host_batch_on_device(int device, const uint8_t *seqs, const int64
     int32_t *d_err = nullptr;
     rc = launch_kind(kind, d_seqs, d_off + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p,
                      d_scores + c0, d_final ? d_final + 7 * (int64_t)c0 : nullptr, d_ws,
-                     ws_bytes, s, true, &d_err);
+                     ws_bytes, s, LAP_STREAM, &d_err);
     if (rc == TSA_OK && d_err) {  // lap kernel: a timed-out hand-off invalidates the chunk
       int32_t herr = 0;
       HIPCHK(hipMemcpyAsync(&herr, d_err, sizeof(herr), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
-      if (herr)
+      if (herr) {
+        // rescore with the helix kernel, which has no cross-workgroup
+        // dependency and cannot time out
+        g_lap_fallbacks.fetch_add(1);
+        fprintf(stderr, "trialign: lap hand-off timed out on device %d (%d triples); rescoring "
+                        "with the helix kernel\n", device, cn);
+        int32_t *d_err2 = nullptr;
         rc = launch_kind(kind, d_seqs, d_off + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p,
-                         d_scores + c0, nullptr, d_ws, ws_bytes, s, false, nullptr);
+                         d_scores + c0, nullptr, d_ws, ws_bytes, s, LAP_OFF, &d_err2);
+        if (rc == TSA_OK && d_err2) rc = TSA_EINTERNAL;  // LAP_OFF never plans a lap grid
+      }
     }
   }
   if (rc) goto done;
@@ -310,6 +336,8 @@ int tsa_score_gpu_ex(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
   const int32_t k = final_states ? TSA_KERNEL_PLANE : kernel;
   return run_host_batch_on_device(device, seqs.data(), off, 0, 1, p, k, score, final_states);
 }
+
+int64_t tsa_fallback_count(void) { return g_lap_fallbacks.load(); }
 
 int tsa_score_gpu(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb, const uint8_t *c,
                   int32_t lc, const tsa_params *p, int32_t *score, int32_t device) {
@@ -426,7 +454,8 @@ int tsa_describe_plan(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
   KParams kp;
   build_kparams(p, &kp);
   pencil_describe(std::min(n, 65535), max_la, max_lb, max_lc, kp,
-                  value_bound(p, max_la, max_lb, max_lc), sync != 0, buf, len);
+                  value_bound(p, max_la, max_lb, max_lc), sync ? LAP_STREAM : LAP_RESIDENT, buf,
+                  len);
   return TSA_OK;
 }
 
@@ -436,7 +465,7 @@ int tsa_batch_workspace_size(int32_t n, int32_t max_la, int32_t max_lb, int32_t 
   if (kernel < TSA_KERNEL_AUTO || kernel > TSA_KERNEL_PENCIL) return TSA_EINVAL;
   const int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
   if (kind < 0) return TSA_ERANGE;
-  *bytes = workspace_for(kind, n, max_la, max_lb, max_lc);
+  *bytes = workspace_for(kind, n, max_la, max_lb, max_lc, p);
   return TSA_OK;
 }
 
@@ -455,11 +484,11 @@ int tsa_score_batch_async(const uint8_t *d_seqs, const int64_t *d_offsets, int32
   }
   const int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
   if (kind < 0) return TSA_ERANGE;
-  if (workspace_bytes < workspace_for(kind, n, max_la, max_lb, max_lc)) return TSA_ENOMEM;
+  if (workspace_bytes < workspace_for(kind, n, max_la, max_lb, max_lc, p)) return TSA_ENOMEM;
   hipStream_t s = (hipStream_t)stream;
   for (int32_t c0 = 0; c0 < n; c0 += 65535) {
     const int32_t cn = std::min<int32_t>(65535, n - c0);
-    const size_t wsz = workspace_for(kind, cn, max_la, max_lb, max_lc);
+    const size_t wsz = workspace_for(kind, cn, max_la, max_lb, max_lc, p);
     int rc = launch_kind(kind, d_seqs, d_offsets + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p,
                          d_scores + c0, nullptr, d_workspace, wsz, s);
     if (rc) return rc;

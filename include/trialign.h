@@ -56,6 +56,12 @@ extern "C" {
 #define TSA_ENOMEM (-5)    /* device allocation failed / workspace too small  */
 #define TSA_EINTERNAL (-6) /* kernel self-check failed                        */
 
+/* Score reported for a triple the device could not score (a lap-kernel
+ * hand-off timed out on tsa_score_batch_async): rescore it. Never a valid
+ * score -- every valid score fits 16 bits. The synchronous entry points
+ * rescore such triples themselves (tsa_fallback_count counts it). */
+#define TSA_SCORE_INVALID INT32_MIN
+
 #define TSA_S3_RTL 0 /* temp_ABC as the RTL evaluates it (src/PE_1cyc.v:162) */
 #define TSA_S3_SOP 1 /* sum of the three pair scores                          */
 
@@ -70,8 +76,8 @@ typedef struct tsa_params {
   int32_t gap_open;   /* GO         (src/PE_1cyc.v:57), default  2 */
   int32_t gap_extend; /* GE         (src/PE_1cyc.v:58), default  1 */
   int32_t s3_mode;    /* TSA_S3_RTL (default) or TSA_S3_SOP          */
-  int32_t score_bits; /* 12 = RTL SCORE_BITS wrap (default); 0 = no wrap;
-                         13..16 also accepted                         */
+  int32_t score_bits; /* 12 = RTL SCORE_BITS wrap (default); 0 = no wrap
+                         (int16 range); any of 4..16 is accepted      */
 } tsa_params;
 
 /* Fill *p with the RTL's effective constants (1, -1, 2, 1, RTL s3, 12 bits). */
@@ -108,7 +114,11 @@ int tsa_score_batch(const uint8_t *seqs, const int64_t *offsets, int32_t n,
  * current device; stream is a hipStream_t (NULL = default stream). The
  * workspace must hold tsa_batch_workspace_size() bytes. max_l* bound every
  * triple's lengths. Launches only; no host synchronisation. Validation of
- * symbols is the caller's job on this path (tsa_validate on the host copy). */
+ * symbols is the caller's job on this path (tsa_validate on the host copy).
+ * For a few large cubes this path may run the single-cube (lap) kernel, whose
+ * workgroups hand data to each other; it only does so when the whole grid is
+ * co-resident, and if a hand-off still times out the affected triples read
+ * TSA_SCORE_INVALID once the stream has synchronised -- check for it. */
 int tsa_batch_workspace_size(int32_t n, int32_t max_la, int32_t max_lb,
                              int32_t max_lc, const tsa_params *p,
                              int32_t kernel, size_t *bytes);
@@ -152,6 +162,11 @@ int tsa_align_gpu(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
 int tsa_describe_plan(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
                       const tsa_params *p, int32_t kernel, int32_t sync, char *buf,
                       size_t len);
+
+/* Lap-kernel hand-offs that timed out on the synchronous entry points since
+ * the library was loaded; each was rescored with the helix kernel (and logged
+ * to stderr). 0 in a healthy run. */
+int64_t tsa_fallback_count(void);
 
 /* Number of visible HIP devices (0 when none), or a negative code. */
 int tsa_device_count(void);

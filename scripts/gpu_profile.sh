@@ -4,7 +4,7 @@
 # MI355X_MICROARCH.md prescribes) and for VALU instructions (SQ_INSTS_VALU). Outputs under gpurun_out/prof_<tag>/.
 set -o pipefail
 R="$GRAFT_REPO_ROOT"
-TAG=${TAG:-r1}
+TAG=${TAG:-r2}
 cd /tmp && export TMPDIR=/tmp
 for k in ${KERNELS:-pencil plane}; do
   OUT="$R/gpurun_out/prof_${TAG}/$k"

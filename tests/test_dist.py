@@ -74,3 +74,40 @@ def test_shard_ranges_cover_exactly(tsa):
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
             assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+
+
+@pytest.mark.parametrize("per_gpu", [3, 4])
+def test_bench_spawn_world2_gloo(tsa, orc, per_gpu):
+    """bench.py's own N>1 path: spawn_ranks starts 2 rank processes with the
+    torch.distributed env set, run_rank shards contiguously, times between
+    barriers, takes the max over ranks and all-gathers the scores; rank 0
+    prints one JSON line with n_gpus 2. The oracle scores each rank's block
+    (CPU stand-in for the GPU, tests/_bench_cpu_rank.py)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "_bench_cpu_rank.py"),
+                        "--gpus", "2", "--per-gpu", str(per_gpu), "--length", "12",
+                        "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["world_size"] == 2
+    assert rec["config"]["triples_total"] == 2 * per_gpu and rec["scaling"] == "weak"
+    assert rec["steps"] == 2 and rec["value"] > 0
+    assert rec["gathered"] == rec["oracle"] and len(rec["gathered"]) == 2 * per_gpu
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)

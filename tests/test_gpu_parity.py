@@ -269,10 +269,16 @@ def test_pencil_lap_streaming_batch(gpu, orc, monkeypatch, tmp_path):
         la, lc = int(rng.integers(100, 129)), int(rng.integers(1, 129))
         triples.append(tuple(rng.integers(0, 4, n).astype(np.uint8) for n in (la, 128, lc)))
     seqs, offs = gpu.pack_batch(triples)
+    before = gpu.fallback_count()
     assert np.array_equal(gpu.score_batch(triples),
                           orc.score_batch(seqs, offs, nthreads=8))
     rows = trace.read_text().splitlines()
-    assert len(rows) - 1 == 800
+    plan = gpu.describe_plan(len(triples), 129, 128, 128, sync=True)
+    kv = dict(f.split("=") for f in plan.split() if "=" in f)
+    m, nw = int(kv["M"]), int(kv["NW"])
+    want = sum(-(-128 // (2 * nw)) * -(-len(t[2]) // (64 * m)) for t in triples)
+    assert int(kv["waves"]) > 1 and len(rows) - 1 == want, (plan, len(rows) - 1, want)
+    assert gpu.fallback_count() == before, "a lap hand-off timed out and was rescored"
 
 
 def test_pencil_ragged_batch(gpu, orc):
@@ -356,3 +362,108 @@ def test_pencil_two_triples_per_wave(gpu, orc, monkeypatch, two):
         ref = orc.score_batch(seqs, offs, orc.default_params(**kw), nthreads=8)
         got = gpu.score_batch(triples, gpu.TsaParams.default(**kw))
         assert np.array_equal(got, ref), (two, kw, arith)
+
+
+# ---- round 2: configs[4] shard, the RTL's largest cubes, lap failure path ----
+
+def test_configs4_full_shard_sampled(gpu, orc, synth):
+    """configs[4]'s per-GPU shard exactly as bench.py runs it: 512 independent
+    256^3 triples resident in HBM, one tsa_score_batch_async launch on torch's
+    stream; >= 16 triples spread over the shard (both ends included) against
+    the oracle, every score in range."""
+    import torch
+    n, L = 512, 256
+    seqs, offs = synth.batch(0, n, L)
+    d_seqs, d_offs = torch.from_numpy(seqs).cuda(), torch.from_numpy(offs).cuda()
+    d_scores = torch.full((n,), -7777, dtype=torch.int32, device="cuda")
+    ws = gpu.workspace_size(n, L, L, L)
+    d_ws = torch.empty(ws, dtype=torch.uint8, device="cuda")
+    assert gpu.describe_plan(n, L, L, L, sync=False).startswith("pencil helix f16")
+    gpu.score_batch_async(d_seqs.data_ptr(), d_offs.data_ptr(), n, L, L, L, d_scores.data_ptr(),
+                          d_ws.data_ptr(), ws, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = d_scores.cpu().numpy()
+    idx = sorted(set([0, 1, n - 2, n - 1] + [int(v) for v in np.linspace(0, n - 1, 16)]))
+    cs, co = gpu.pack_batch([synth.triple(i, L) for i in idx])
+    ref = orc.score_batch(cs, co, nthreads=16)
+    assert np.array_equal(got[idx], ref), (idx, got[idx], ref)
+    assert got.min() > -3 * L - 16 and got.max() <= 3 * L  # value bound, no sentinel left
+
+
+@pytest.mark.parametrize("kind", ["random", "all_a", "all_mismatch", "related"])
+def test_512_cube_rtl_params(gpu, orc, synth, kind):
+    """The RTL's largest input (A_TOTAL_LEN = 512, src/TriAlign_1cyc.v:7) with
+    its 12-bit words: the value bound [-1544, 1536] fits 12 bits, so AUTO runs
+    the pencil path (factored f16 form) and must equal the literal oracle --
+    including the cubes at the two ends of the bound."""
+    L = 512
+    if kind == "random":
+        a, b, c = synth.triple(5, L)
+    elif kind == "all_a":          # the upper end: 3 per diagonal step -> 1536
+        a = b = c = np.zeros(L, np.uint8)
+    elif kind == "all_mismatch":   # a != b != c everywhere: the low side
+        a, b, c = (np.full(L, v, np.uint8) for v in (0, 1, 2))
+    else:
+        a, b, c = synth.related_triple(11, L)
+    assert gpu.describe_plan(1, L, L, L).startswith("pencil ")
+    got = gpu.score(a, b, c)
+    assert got == orc.score(a, b, c), kind
+    if kind == "all_a":
+        assert got == 3 * L
+
+
+def test_lap_timeout_is_reported_not_silent(gpu, orc, synth, monkeypatch):
+    """Injected lap hand-off timeout (TSA_LAP_SPIN_LIMIT=0: the first poll of
+    every consumer gives up): the async path marks the triple
+    TSA_SCORE_INVALID; the synchronous path counts the fallback, rescored the
+    chunk with the helix kernel and still returns the exact score."""
+    import torch
+    L = 256
+    a, b, c = synth.triple(2, L)
+    ref = orc.score(a, b, c)
+    monkeypatch.setenv("TSA_LAP_SPIN_LIMIT", "0")
+    assert gpu.describe_plan(1, L, L, L, sync=False).startswith("pencil lap")
+    seqs, offs = gpu.pack_batch([(a, b, c)])
+    d_seqs, d_offs = torch.from_numpy(seqs).cuda(), torch.from_numpy(offs).cuda()
+    d_score = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ws = gpu.workspace_size(1, L, L, L)
+    d_ws = torch.empty(ws, dtype=torch.uint8, device="cuda")
+    gpu.score_batch_async(d_seqs.data_ptr(), d_offs.data_ptr(), 1, L, L, L, d_score.data_ptr(),
+                          d_ws.data_ptr(), ws, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert int(d_score.item()) == gpu.SCORE_INVALID
+    before = gpu.fallback_count()
+    assert gpu.score(a, b, c) == ref
+    assert gpu.fallback_count() == before + 1
+    monkeypatch.delenv("TSA_LAP_SPIN_LIMIT")
+    gpu.score_batch_async(d_seqs.data_ptr(), d_offs.data_ptr(), 1, L, L, L, d_score.data_ptr(),
+                          d_ws.data_ptr(), ws, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert int(d_score.item()) == ref
+    assert gpu.score(a, b, c) == ref and gpu.fallback_count() == before + 1
+
+
+@pytest.mark.parametrize("m,nw", [(1, 4), (1, 8), (2, 4), (2, 8), (4, 4), (4, 8)])
+def test_lap_kernel_geometries_adversarial(gpu, orc, monkeypatch, m, nw):
+    """Every (M, NW) geometry of the lap kernel on cubes whose optimum runs
+    through lap and tile seams: all-mismatch (values near the low bound; the
+    seam cell (1, y, 64M+1) takes its step-0 inputs from the left tile's
+    records ZT-2 / ZT-1), all-match, related and random, ragged shapes."""
+    monkeypatch.setenv("TSA_PENCIL_MODE", "lap")
+    monkeypatch.setenv("TSA_LAP_M", str(m))
+    monkeypatch.setenv("TSA_LAP_NW", str(nw))
+    rng = np.random.default_rng(100 * m + nw)
+    for la, lb, lc in [(100, 100, 100), (130, 70, 300), (64, 33, 129), (200, 41, 257), (17, 90, 65)]:
+        for kind in ("mismatch", "match", "related", "random"):
+            if kind == "mismatch":
+                a, b, c = (np.full(n, v, np.uint8) for n, v in zip((la, lb, lc), (0, 1, 2)))
+            elif kind == "match":
+                a, b, c = (np.zeros(n, np.uint8) for n in (la, lb, lc))
+            elif kind == "related":
+                base = rng.integers(0, 4, max(la, lb, lc)).astype(np.uint8)
+                a, b, c = base[:la].copy(), base[:lb].copy(), base[:lc].copy()
+                b[::7] = (b[::7] + 1) % 4
+                c[::5] = (c[::5] + 2) % 4
+            else:
+                a, b, c = (rng.integers(0, 4, n).astype(np.uint8) for n in (la, lb, lc))
+            assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (m, nw, la, lb, lc, kind)

@@ -64,3 +64,58 @@ def test_synth_batch_layout(synth):
     a, b, c = synth.triple(4, 10, 12, 14)
     assert np.array_equal(seqs[offs[3]:offs[4]], a)
     assert np.array_equal(seqs[offs[5]:offs[6]], c)
+
+
+def test_pencil_exact_dispatch_bounds(tsa):
+    """pencil_exact: the 12-bit RTL wrap is checked against the bare value
+    bound and the carrier against the bound plus a few penalties -- pencil up
+    to 680 per side with 12-bit words, exact f16 up to ~676, the literal plane
+    kernel beyond."""
+    for L, want in [(256, "pencil"), (512, "pencil"), (600, "pencil"), (680, "pencil"),
+                    (681, "plane"), (1024, "plane")]:
+        assert tsa.describe_plan(1, L, L, L).split()[0] == want, L
+    assert " f16 " in tsa.describe_plan(1, 512, 512, 512)
+    assert " i16 " in tsa.describe_plan(1, 680, 680, 680)
+
+
+def test_ram128_image_round_trip(tsa, tmp_path):
+    """The testbench's sequence RAM (src/TriAlign_tb.sv:94-96,149-169): 32
+    four-bit symbols per 128-bit word, symbol i at bits [4(i%32)+3 : 4(i%32)]
+    of word i/32 -- packed, as $readmemh text, as raw words."""
+    rng = np.random.default_rng(3)
+    for n in (1, 31, 32, 33, 64, 100):
+        s = rng.integers(0, 5, n).astype(np.uint8)
+        w = tsa.pack_ram128(s)
+        assert w.shape == ((n + 31) // 32, 16)
+        assert np.array_equal(tsa.unpack_ram128(w, n), s)
+        # nibble placement: symbol i of word 0 is bits [4i+3:4i] of the 128-bit word
+        word0 = int.from_bytes(bytes(w[0]), "little")
+        assert all(((word0 >> (4 * i)) & 15) == s[i] for i in range(min(n, 32)))
+        hx = tmp_path / f"s{n}.hex"
+        hx.write_text("\n".join(tsa.ram128_hex_lines(s)) + "\n")
+        assert np.array_equal(tsa.read_sequence(str(hx), "ramhex", n), s)
+        raw = tmp_path / f"s{n}.bin"
+        w.tofile(str(raw))
+        assert np.array_equal(tsa.read_sequence(str(raw), "ramraw", n), s)
+    with pytest.raises(tsa.TsaError):
+        tsa.unpack_ram128(np.zeros((1, 16), np.uint8), 33)
+
+
+def test_testbench_initial_block_reader(tsa, orc, tmp_path):
+    """The testbench's own input format: `seqA_ram[w][hi:lo] <= SYM;` writes in
+    an initial block (src/TriAlign_tb.sv:423-1960). A synthetic block in that
+    form round-trips; when the reference tree is present its testbench is read
+    directly -- all-A, A_LENGTH = 64 (src/TriAlign_tb.sv:48) -> score 192."""
+    rng = np.random.default_rng(4)
+    s = rng.integers(0, 5, 70).astype(np.uint8)
+    names = "ATCGN"
+    lines = [f"seqB_ram[{i // 32}][{4 * (i % 32) + 3}:{4 * (i % 32)}] <= {names[v]};"
+             for i, v in enumerate(s)]
+    f = tmp_path / "tb.sv"
+    f.write_text("initial begin\n" + "\n".join(lines) + "\nend\n")
+    assert np.array_equal(tsa.read_sequence(str(f), ram="seqB_ram"), s)
+    tb = "/root/reference/src/TriAlign_tb.sv"
+    if os.path.exists(tb):
+        seqs = [tsa.read_sequence(tb, ram=f"seq{k}_ram", length=64) for k in "ABC"]
+        assert all(len(x) == 64 and not x.any() for x in seqs)
+        assert orc.score(*seqs) == 192

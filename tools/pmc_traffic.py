@@ -23,6 +23,8 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import kernel_source_hash  # noqa: E402  (the stamp bench.py checks)
 
 
 def rows(path):
@@ -92,6 +94,7 @@ def main(tag="r1"):
                                "avg_ns": big["avg_ns"], "hbm_bytes_per_launch": big["hbm_bytes_corrected"],
                                "hbm_bytes_raw": big["hbm_bytes_raw"],
                                "valu_insts_per_launch": big.get("valu_insts"),
+                               "kernel_source_sha256": kernel_source_hash(kn),
                                "note": "(2*FETCH_SIZE+WRITE_SIZE)*1024, gfx950 FETCH_SIZE correction"},
                               f, indent=1)
     with open(os.path.join(outdir, f"{tag}_profile_summary.json"), "w") as f:
