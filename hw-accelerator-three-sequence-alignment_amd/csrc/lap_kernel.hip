@@ -52,7 +52,7 @@
 namespace tsa {
 
 #ifndef TSA_LAP_PD1  // LDS-DMA prefetch distance (steps) by M: build-time knobs
-#define TSA_LAP_PD1 8
+#define TSA_LAP_PD1 3
 #endif
 #ifndef TSA_LAP_PD2
 #define TSA_LAP_PD2 6
@@ -68,7 +68,15 @@ constexpr int LAP_PUB = 4;         // consumers publish their progress every LAP
 constexpr int LAP_PROG_STRIDE = 32;  // progress words 128 B apart (one line each)
 constexpr int LAP_ZREC_WAVE = 32;  // z record bytes per wave: 4 x {payload, tag}
 
-static_assert(LAP_ZL > TSA_LAP_PD1 + 2 && LAP_ZL > TSA_LAP_PD2 + 2, "z slots");
+#ifndef TSA_LAP_SKEW  // steps between a wave's high row and the next wave's low row
+#define TSA_LAP_SKEW 1
+#endif
+// SK = 1: one barrier per step, the wave below reads this step's record next
+// step; SK = 2: a wave reads the record of two steps ago, one barrier per two
+// steps (tools/lap_emu.py replays both)
+constexpr int LAP_SK = TSA_LAP_SKEW;
+static_assert(LAP_SK == 1 || LAP_SK == 2, "lap skew");
+static_assert(LAP_ZL > TSA_LAP_PD1 + 2 + LAP_SK && LAP_ZL > TSA_LAP_PD2 + 2 + LAP_SK, "z slots");
 
 // Tag of the record of step s in the launch with epoch e (32-bit): distinct
 // steps of one launch never collide (odd multiplier).
@@ -78,9 +86,9 @@ __host__ __device__ __forceinline__ uint32_t lap_tag(uint32_t e, int32_t s) {
 
 static size_t lap_lds_bytes(int M, int NW, int32_t max_la) {
   const int ZT = 64 * M, SLOT = M * 1024;
-  return (size_t)(NW - 1) * 2 * SLOT + (size_t)lap_pd(M) * SLOT + 4 * (size_t)NW * 16 +
+  return (size_t)(NW - 1) * 2 * LAP_SK * SLOT + (size_t)lap_pd(M) * SLOT + 4 * (size_t)NW * 16 +
          (size_t)LAP_ZL * NW * LAP_ZREC_WAVE + 16 + (size_t)M * 256 +
-         4 * (((size_t)max_la + 2 * ZT + 4 * NW + 8) & ~(size_t)3);
+         4 * (((size_t)max_la + 2 * ZT + 2 * (LAP_SK + 1) * NW + 8 + 3) & ~(size_t)3);
 }
 
 // ---------------------------------------------------------------------------
@@ -113,7 +121,7 @@ __device__ __forceinline__ int32_t lds_word(const int32_t *p) {
 }
 
 // LDS (bytes):
-//   xr    [NW-1][2][M][64][16]  wave w -> w+1 records {Iy, Ixy, Iyz, best}
+//   xr    [NW-1][2SK][M][64][16] wave w -> w+1 records {Iy, Ixy, Iyz, best}
 //   xr0   [LPD][M][64][16]      tagged y records of the lap above (LDS-DMA)
 //   zst   [4][NW][16]           z staging {Iz, Ixz, REC.z, REC.w} of lane 63
 //   zring [ZL][NW][32]          tagged z records of the tile to the left
@@ -141,9 +149,12 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int RW = 2 * NW, ZT = 64 * M, LPD = lap_pd(M);
   constexpr int PAIR = 64 * REC_BYTES, SLOT = M * PAIR;
-  constexpr int ZREC = NW * LAP_ZREC_WAVE, OFF = ZT + 2 * NW;
+  // wave w's rows sit at step offsets WO*w (low half) and WO*w + 1 (high);
+  // lap L+1 reads lap L's record t + YOFF; z records are checked ZV steps ahead
+  constexpr int SK = LAP_SK, WO = SK + 1, NSL = 2 * SK, YOFF = WO * (NW - 1) + 1, ZV = SK;
+  constexpr int ZREC = NW * LAP_ZREC_WAVE, OFF = ZT + WO * NW;
   uint8_t *xr = smem;
-  uint8_t *xr0 = xr + (NW - 1) * 2 * SLOT;
+  uint8_t *xr0 = xr + (NW - 1) * NSL * SLOT;
   uint8_t *zst = xr0 + LPD * SLOT;
   uint8_t *zring = zst + 4 * NW * 16;
   int32_t *bpw = (int32_t *)(zring + LAP_ZL * ZREC);
@@ -182,10 +193,11 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
   const bool yin = L > 0, zin = q > 0, yout = L + 1 < nlap, zout = q + 1 < ntile;
   const int32_t zt_q = min(ZT, lc - q * ZT), rows = min(RW, lb - L * RW);
   const bool final_wg = !yout && !zout;
+  auto tau = [](int32_t r) { return WO * (r >> 1) + (r & 1); };  // step offset of lap row r
   const int32_t r_f = lb - 1 - L * RW, k_f = lc - 1 - q * ZT;
-  const int32_t T = final_wg ? (la - 1) + r_f + k_f + 1 : la + rows + zt_q - 2;
-  const int32_t T_above = la + RW + zt_q - 2;  // records the lap above writes (same tile)
-  const int32_t T_left = la + rows + ZT - 2;   // z records the tile to the left writes
+  const int32_t T = final_wg ? (la - 1) + tau(r_f) + k_f + 1 : la + tau(rows - 1) + zt_q - 1;
+  const int32_t T_above = la + tau(RW - 1) + zt_q - 1;  // records the lap above writes (same tile)
+  const int32_t T_left = la + tau(rows - 1) + ZT - 1;   // z records the tile to the left writes
   uint8_t *yf_mine = yf_base + lid * YR * SLOT;
   const uint8_t *yf_prev = yin ? yf_base + (lid - GZ) * YR * SLOT : yf_mine;
   uint8_t *zf_mine = zf_base + lid * ZR * ZREC;
@@ -199,16 +211,16 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
   };
 
   // ---- A code pairs, per-row and per-position registers
-  const int32_t na = la + 2 * ZT + 4 * NW + 8;
+  const int32_t na = la + 2 * ZT + 2 * WO * NW + 8;
   for (int j = threadIdx.x; j < na; j += 64 * NW) {
     const int x0 = j - OFF, x1 = j - OFF - 1;
     const uint32_t c0 = (x0 >= 0 && x0 < la) ? SYM0 << (seqs[o0 + x0] & 3) : 0u;
     const uint32_t c1 = (x1 >= 0 && x1 < la) ? SYM0 << (seqs[o0 + x1] & 3) : 0u;
     sA2[j] = c0 | (c1 << 16);
   }
-  // a[i] of this lane at step t = sA2[t - 2w - (M lane + i) + OFF]
+  // a[i] of this lane at step t = sA2[t - WO w - (M lane + i) + OFF]
   const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
-                          4u * (uint32_t)(OFF - 2 * w - M * lane - (M - 1));
+                          4u * (uint32_t)(OFF - WO * w - M * lane - (M - 1));
   const int32_t y0 = L * RW + 2 * w;  // rows y0 (lo) and y0 + 1 (hi), 0-based
   const uint32_t bw = (y0 < lb ? SYM0 << (seqs[o1 + y0] & 3) : 0u) |
                       ((y0 + 1 < lb ? SYM0 << (seqs[o1 + y0 + 1] & 3) : 0u) << 16);
@@ -265,8 +277,8 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
   };
 
   // ---- consumer side (wave 0): fetches, tag checks
-  auto fetch_y = [&](int32_t s) {  // records of step s (row s + RW - 1 above) -> xr0 slot s % LPD
-    const int32_t r = s + RW - 1;
+  auto fetch_y = [&](int32_t s) {  // records of step s (row s + YOFF above) -> xr0 slot s % LPD
+    const int32_t r = s + YOFF;
 #pragma unroll
     for (int i = 0; i < M; ++i)
       dma16(yf_prev + ((int64_t)(r & (YR - 1)) * M + i) * PAIR + lane * REC_BYTES,
@@ -309,23 +321,20 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
 
   // prologue (wave 0): z records ZT-2 and ZT-1 (what the shifts of steps -2 and
   // -1 would have brought into position 0: its Iz/Iyz inputs of step 0 and its
-  // Ixz/M inputs of steps 0 and 1) and ZT (step 0's shift); then LPD steps of y
-  // and z fetches -- M + 1 DMAs per step, always (dummy ones where there is no
-  // producer), so the per-step vmcnt count is a constant
+  // Ixz/M inputs of steps 0 and 1) and ZT .. ZT+ZV-1 (the shifts before the
+  // first check); then LPD steps of y and z fetches -- M + 1 DMAs per step,
+  // always (dummy ones where there is no producer), so the per-step vmcnt count
+  // is a constant
   if (w == 0) {
     if (lane < 4) bpw[lane] = 0;
     if (zin) {
-      fetch_z(ZT - 2);
-      fetch_z(ZT - 1);
-      fetch_z(ZT);
+      for (int rz = ZT - 2; rz < ZT + ZV; ++rz) fetch_z(rz);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      settle_z(ZT - 2);
-      settle_z(ZT - 1);
-      settle_z(ZT);
+      for (int rz = ZT - 2; rz < ZT + ZV; ++rz) settle_z(rz);
     }
     for (int s = 0; s < LPD; ++s) {
       fetch_y(s);
-      fetch_z(s + ZT + 1);
+      fetch_z(s + ZT + ZV);
     }
   }
   __syncthreads();
@@ -362,7 +371,7 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
     if constexpr (ROLE == 0) {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"((M + 1) * (LPD - 1)) : "memory");
       if (yin) {
-        const int32_t r = t + RW - 1;
+        const int32_t r = t + YOFF;
         uint4 rv[M];
         const uint8_t *src = xr0 + (t % LPD) * SLOT + lane * REC_BYTES;
 #pragma unroll
@@ -396,9 +405,9 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
           Rb[i] = rows2(pBest[i], face.w);
         }
       }
-      settle_z(t + ZT + 1);  // the z record all waves shift in after this step's barrier
-    } else {
-      const uint8_t *src = xr + ((w - 1) * 2 + (PH ^ 1)) * SLOT + lane * REC_BYTES;
+      settle_z(t + ZT + ZV);  // the z record all waves shift in ZV steps from now
+    } else {  // the record wave w-1 wrote SK steps ago
+      const uint8_t *src = xr + ((w - 1) * NSL + ((t + NSL - SK) & (NSL - 1))) * SLOT + lane * REC_BYTES;
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         const uint4 rv = lds_read16(src + i * PAIR);
@@ -421,7 +430,7 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
     }
     // ---- x = 1: low half at position t - 2w, high half one position behind;
     // their x - 1 inputs are the x = 0 face (src/PE_1cyc.v:164-178,196-218)
-    const int32_t klo = __builtin_amdgcn_readfirstlane(t - 2 * w);  // uniform: SGPR lane masks
+    const int32_t klo = __builtin_amdgcn_readfirstlane(t - WO * w);  // uniform: SGPR lane masks
     if (klo >= 0 && klo <= ZT) {
       const int32_t khi = klo - 1;
       const uint64_t lm_lo = sgpr64(klo < ZT ? 1ull << (klo / M) : 0ull);
@@ -457,7 +466,7 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
                                     nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (FIN) {  // the final cell (src/TriAlign_1cyc.v:141-142,342-345)
-      if (final_wg && w == (r_f >> 1)) {
+      if (final_wg && w == (r_f >> 1)) {  // row r_f: half r_f & 1 of wave r_f / 2
 #pragma unroll
         for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
       }
@@ -468,13 +477,13 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
                   make_uint4(oIz[M - 1], oIxz[M - 1], Ryz[M - 1], Rb[M - 1]));
     // ---- records: to the wave below, or (last wave) the y ring and z ring
     if constexpr (ROLE != 2) {
-      uint8_t *dst = xr + (w * 2 + PH) * SLOT + lane * REC_BYTES;
+      uint8_t *dst = xr + (w * NSL + (t & (NSL - 1))) * SLOT + lane * REC_BYTES;
 #pragma unroll
       for (int i = 0; i < M; ++i)
         lds_write16(dst + i * PAIR, make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
     } else {
       if (yout) {
-        wait_consumer(cons_y, seen_y, bpw, t - YR - RW + 1);
+        wait_consumer(cons_y, seen_y, bpw, t - YR - YOFF);
         const uint32_t tg = lap_tag(epoch, t);
 #pragma unroll
         for (int i = 0; i < M; ++i)
@@ -482,9 +491,9 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
                       make_uint4(perm(oIxy[i], oIy[i], 0x07060302u), tg,
                                  perm(oBest[i], oIyz[i], 0x07060302u), tg));
       }
-      if (zout && t >= 1) {  // z record of step t-1: complete in LDS since the last barrier
-        const int32_t s = t - 1;
-        wait_consumer(cons_z, seen_z, bpw + 1, s - ZR - ZT - 1);
+      if (zout && t >= SK) {  // z record of step t-SK: complete in LDS since the last barrier
+        const int32_t s = t - SK;
+        wait_consumer(cons_z, seen_z, bpw + 1, s - ZR - ZT - ZV);
         if (lane < 2 * NW) {
           const uint32_t tg = lap_tag(epoch, s);
           const uint4 v = lds_read16(zst + ((s & 3) * NW + (lane >> 1)) * 16);
@@ -523,17 +532,17 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
     zshift<M>(svM[PH], Rb, sel0, fM);
     if constexpr (ROLE == 0) {
       fetch_y(t + LPD);
-      fetch_z(t + LPD + ZT + 1);
+      fetch_z(t + LPD + ZT + ZV);
     }
-    // progress of this workgroup as a consumer: by the last barrier wave 0 had
-    // landed and checked the y records <= (t-1) + RW - 1 and the z records
-    // <= (t-1) + ZT + 1; published as t (decoded: step t-1 complete)
+    // progress of this workgroup as a consumer: by the last barrier (t-1 is
+    // odd) wave 0 had landed and checked the y records <= (t-1) + YOFF and the z
+    // records <= (t-1) + ZT + ZV; published as t (decoded: step t-1 complete)
     if constexpr (ROLE == 1) {
       if (w == 1 && (t & (LAP_PUB - 1)) == 0 && lane == 0 && (yin || zin))
         __hip_atomic_store(prog + lid * LAP_PROG_STRIDE, (int32_t)((ep19 << 13) | (uint32_t)t),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr (SK == 1 || PH == 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
   auto run = [&](auto role) {  // the last step peeled off (it records the final cell)
     int32_t t = 0;
@@ -565,14 +574,16 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
       trace[(int64_t)b * 8 + 5] = n_bp;
     }
   }
-  // the z record of the last step: staged before the loop's final barrier
+  // the z records of the last SK steps and the final cell: staged before this barrier
+  __syncthreads();
   if (w == NW - 1 && zout && lane < 2 * NW) {
-    const int32_t s = T - 1;
-    wait_consumer(cons_z, seen_z, bpw + 1, s - ZR - ZT - 1);
-    const uint32_t tg = lap_tag(epoch, s);
-    const uint4 v = lds_read16(zst + ((s & 3) * NW + (lane >> 1)) * 16);
-    const uint4 o = (lane & 1) ? make_uint4(v.z, tg, v.w, tg) : make_uint4(v.x, tg, v.y, tg);
-    store16_sc1(zf_mine + (int64_t)(s & (ZR - 1)) * ZREC + lane * 16, o);
+    for (int32_t s = max(T - SK, 0); s < T; ++s) {
+      wait_consumer(cons_z, seen_z, bpw + 1, s - ZR - ZT - ZV);
+      const uint32_t tg = lap_tag(epoch, s);
+      const uint4 v = lds_read16(zst + ((s & 3) * NW + (lane >> 1)) * 16);
+      const uint4 o = (lane & 1) ? make_uint4(v.z, tg, v.w, tg) : make_uint4(v.x, tg, v.y, tg);
+      store16_sc1(zf_mine + (int64_t)(s & (ZR - 1)) * ZREC + lane * 16, o);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (final_wg && threadIdx.x == 0) {
@@ -628,13 +639,14 @@ static int lap_blocks_per_cu_t(size_t lds) {
                : ((NW_) == 4 ? TSA_ARITH(FN, 4, 4, F16_, SOP_, __VA_ARGS__)                    \
                              : TSA_ARITH(FN, 4, 8, F16_, SOP_, __VA_ARGS__)))
 
-// Measured per-step times (us) of one workgroup, no hand-off stalls, by M and
-// waves per SIMD (NW/4 for a lone workgroup, more when several share a CU).
-static double lap_step_us(int M, int waves_per_simd) {
-  const double base = M == 1 ? 0.14 : M == 2 ? 0.22 : 0.40;
-  return base * (waves_per_simd <= 1 ? 1.0 : 0.6 * waves_per_simd + 0.1);
+// Step time (us) along the chain, fitted to single-cube runs on MI355X
+// (scripts/gpu_lap.sh): 64^3..512^3 with one workgroup per CU
+// give 0.48-0.56 (M = 1), 0.62-0.67 (M = 2), 0.81 (M = 4); 1024^3 with 2-4
+// workgroups per CU 0.84-0.87 -- the chain steps include the hand-off stalls.
+static double lap_step_us(int M, int NW, int64_t wg_per_cu) {
+  const double base = M == 1 ? (NW == 4 ? 0.50 : 0.52) : M == 2 ? 0.65 : 0.82;
+  return base * (1.0 + 0.22 * (double)(std::max<int64_t>(wg_per_cu, 1) - 1));
 }
-constexpr double LAP_HOP_US = 2.0;  // tagged-record hand-off: store -> visible -> DMA landed
 
 LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW,
                  bool full_rings, bool f16, bool sop) {
@@ -646,9 +658,10 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   g.GZ = (max_lc + ZT - 1) / ZT;
   g.NC = n * g.GZ;             // columns: (triple, z-tile)
   g.CH = (g.NC + 7) / 8;       // columns per XCD
-  const int32_t T = max_la + RW + ZT;  // >= every workgroup's step count
+  const int YOFF = (LAP_SK + 1) * (NW - 1) + 1;  // lap lag of a record (kernel: YOFF)
+  const int32_t T = max_la + YOFF + ZT;  // >= every workgroup's step count
   auto pow2 = [](int64_t v) { int64_t p = 1; while (p < v) p <<= 1; return (int32_t)p; };
-  g.YR = full_rings ? pow2(T) : pow2(RW + LPD + 48);
+  g.YR = full_rings ? pow2(T) : pow2(YOFF + LPD + 48);
   g.ZR = full_rings ? pow2(T) : pow2(ZT + LPD + 48);
   g.lds = lap_lds_bytes(M, NW, max_la);
   if (const char *e = getenv("TSA_LAP_LDS_EXTRA")) g.lds += (size_t)atoi(e);  // diagnostic knob
@@ -668,15 +681,16 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
                                            (wgs + (int64_t)cus * per_cu - 1) / ((int64_t)cus * per_cu))
                        : 0;
   g.ok = per_cu > 0 && (g.G >= 2 || g.GZ >= 2);
-  // estimated latency (us): the chain to the final workgroup plus its own steps;
-  // several workgroups on one CU share its SIMDs
+  // estimated latency (us): the chain to the final workgroup -- each lap adds
+  // YOFF + LPD + ~3 steps, each tile ZT + LPD + ~2 -- plus its own steps;
+  // several workgroups on one CU share its SIMDs. A grid beyond the resident
+  // slots runs in dispatch waves that barely overlap (~2.8x per wave).
   const int64_t xcd_cus = std::max(1, cus / 8);
   const int64_t wg_cu = std::max<int64_t>(1, std::min<int64_t>(per_cu, (wg_per_xcd + xcd_cus - 1) / xcd_cus));
-  const double st = lap_step_us(M, (int)std::max<int64_t>(1, wg_cu * NW / 4));
-  const double chain = (double)(g.G - 1) * ((RW + LPD) * st + LAP_HOP_US) +
-                       (double)(g.GZ - 1) * ((ZT + LPD) * st + LAP_HOP_US);
-  const double own = (max_la + RW + ZT) * st;
-  g.est_us = g.waves <= 1 ? chain + own : 2.8 * g.waves * (chain + own);
+  const double steps = (double)(g.G - 1) * (YOFF + LPD + 3) + (double)(g.GZ - 1) * (ZT + LPD + 2) +
+                       (double)(max_la + YOFF + ZT);
+  const double chain = steps * lap_step_us(M, NW, wg_cu);
+  g.est_us = g.waves <= 1 ? chain : 2.8 * (double)g.waves * chain;
   return g;
 }
 

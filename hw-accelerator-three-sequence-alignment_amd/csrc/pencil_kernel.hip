@@ -112,10 +112,12 @@ static bool use_f16(const KParams &kp, const Range &r);
 // Estimated latency (us) of the helix kernel for a batch: dispatch waves x
 // steps per triple x step time. Measured: a fully loaded chip (two 8-wave
 // workgroups per CU) runs an M = 2 step in ~0.66 us (512 x 256^3 in 5.6 ms);
-// a workgroup alone on its CU in about 60 % of that.
+// a workgroup alone on its CU in 0.38 us (one 256^3 triple, 3.2 ms), M = 1
+// (two triples per wave) in 0.31 us (one 64^3 triple, 0.18 ms).
 static double helix_step_us(int M, bool loaded) {
   const double s = M == 1 ? 0.40 : M == 2 ? 0.66 : M == 4 ? 1.2 : 2.4;
-  return loaded ? s : 0.6 * s;
+  const double alone = M == 1 ? 0.31 : M == 2 ? 0.38 : M == 4 ? 0.7 : 1.4;
+  return loaded ? s : alone;
 }
 static double helix_est(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
   const PencilGeom g = pencil_geom(max_la, max_lc);

@@ -10,7 +10,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PKG_DIR = os.path.join(ROOT, "hw-accelerator-three-sequence-alignment_amd")
+# TSA_PKG_DIR: run the tests against a variant build (scripts/build_variant.sh)
+PKG_DIR = os.environ.get("TSA_PKG_DIR", os.path.join(ROOT, "hw-accelerator-three-sequence-alignment_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 sys.path.insert(0, ROOT)
 

@@ -86,8 +86,17 @@ def test_describe_plan(tsa):
     p = tsa.TsaParams.default()
     assert tsa.describe_plan(512, 256, 256, 256, p).startswith("pencil helix f16 rtl M=2 NW=8")
     assert tsa.describe_plan(1, 256, 256, 256, p).startswith("pencil lap f16 rtl M=1")
-    assert "waves=2" in tsa.describe_plan(32, 256, 256, 256, p, sync=True)
-    assert tsa.describe_plan(32, 256, 256, 256, p, sync=False).startswith("pencil helix")
+    # a few cubes: the lap kernel; many: the helix; the synchronous path may
+    # stream a lap grid beyond the resident slots (waves > 1), the async one not
+    assert tsa.describe_plan(4, 256, 256, 256, p, sync=False).startswith("pencil lap f16")
+    assert tsa.describe_plan(64, 256, 256, 256, p, sync=False).startswith("pencil helix")
+    import os
+    os.environ["TSA_PENCIL_MODE"] = "lap"
+    try:
+        assert "waves=1" not in tsa.describe_plan(100, 129, 128, 128, p, sync=True)
+        assert tsa.describe_plan(100, 129, 128, 128, p, sync=False).startswith("pencil helix")
+    finally:
+        del os.environ["TSA_PENCIL_MODE"]
     # M = 2 lap periods are even (the x = 1 register is then PH ^ (w & 1))
     assert "M=2 NW=8 P=258" in tsa.describe_plan(512, 257, 40, 255, p)
     assert "M=2 NW=8 P=256" in tsa.describe_plan(512, 255, 40, 255, p)

@@ -19,9 +19,10 @@ CASES = [((20, 11, 70), 2, 1), ((5, 3, 1), 2, 1), ((1, 1, 1), 2, 1), ((30, 9, 13
          ((10, 20, 66), 2, 1), ((20, 40, 70), 2, 1), ((16, 24, 130), 4, 2)]
 
 
+@pytest.mark.parametrize("sk", [1, 2])
 @pytest.mark.parametrize("shape,nw,m", CASES)
 @pytest.mark.parametrize("kind", ["random", "mismatch", "match"])
-def test_lap_schedule_vs_oracle(orc, shape, nw, m, kind):
+def test_lap_schedule_vs_oracle(orc, shape, nw, m, kind, sk):
     la, lb, lc = shape
     rng = np.random.default_rng(la * 7 + lb * 3 + lc)
     if kind == "random":
@@ -32,4 +33,4 @@ def test_lap_schedule_vs_oracle(orc, shape, nw, m, kind):
         a, b, c = (np.zeros(n, np.uint8) for n in shape)
     sop = bool(rng.integers(0, 2))
     op = orc.default_params(score_bits=16, s3_mode=int(sop))
-    assert emulate(a, b, c, sop=sop, NW=nw, M=m) == orc.score(a, b, c, op)
+    assert emulate(a, b, c, sop=sop, NW=nw, M=m, SK=sk) == orc.score(a, b, c, op)

@@ -47,7 +47,7 @@ def codes(seq, n):
     return out
 
 
-def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, cells=None):
+def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, SK=1, cells=None):
     """Score of one triple by the lap schedule (no wrap: valid where the
     factored form is exact)."""
     la, lb, lc = len(a), len(b), len(c)
@@ -60,8 +60,14 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, cel
     s3_ne = 3 * mismatch
     s3_ab = 2 * (match + mismatch)                # src/PE_1cyc.v:162 precedence
     s3_eq = 3 * match
+    # SK: steps between a wave's high row and the next wave's low row (the
+    # kernel reads the wave above's record SK steps old); wave w's rows sit at
+    # step offsets WO*w (low half) and WO*w + 1 (high half), WO = SK + 1
+    WO = SK + 1
+    tau = lambda r: WO * (r >> 1) + (r & 1)
+    YOFF = WO * (NW - 1) + 1           # lap L+1 step t reads lap L's record t + YOFF
     # A table: entry j holds x = j - OFF (lo) and x = j - OFF - 1 (hi)
-    OFF = 2 * NW + ZT
+    OFF = WO * NW + ZT
     yrec = {}   # (L, q) -> list over steps of 4 arrays [M, 64, 2] (last wave's out record)
     zrec = {}   # (L, q) -> list over steps of [NW][4] pairs (lane 63, reg M-1)
     score = None
@@ -70,7 +76,7 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, cel
         for q in range(GZ):
             zt_q = min(ZT, lc - q * ZT)
             rows = min(RW, lb - L * RW)
-            T = la + (rows - 1) + (zt_q - 1)          # last real cell of the WG at step T-1
+            T = la + tau(rows - 1) + (zt_q - 1)       # last real cell of the WG at step T-1
             A = codes(a, la)
             Bc = codes(b, lb)
             Cc = codes(c, lc)
@@ -102,13 +108,14 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, cel
                     shIxz[0, w, 0, 0] = r2[1]
                     svM[0, w, 0, 0] = r2[3]
             ys, zs = [], []
+            out_hist = []
             for t in range(T):
                 PH = t & 1
                 out_now = np.zeros_like(out_prev)
                 zstep = [None] * NW
                 for w in range(NW):
                     # A codes: lo u = t - 2w - k, hi u - 1 (table entry j = u + OFF)
-                    j = t - 2 * w - kpos + OFF
+                    j = t - WO * w - kpos + OFF
                     ulo = j - OFF
                     alo = np.where((ulo >= 0) & (ulo < la), A[np.clip(ulo, 0, la - 1)], 0)
                     ahi = np.where((ulo - 1 >= 0) & (ulo - 1 < la), A[np.clip(ulo - 1, 0, la - 1)], 0)
@@ -122,10 +129,10 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, cel
                             above = np.array(face, np.int64)[:, None, None, None] * np.ones((4, M, 64, 2), np.int64)
                         else:
                             prev = yrec[(L - 1, q)]
-                            r = t + RW - 1
+                            r = t + YOFF
                             above = prev[min(r, len(prev) - 1)]
-                    else:
-                        above = out_prev[:, w - 1]
+                    else:  # the record wave w-1 wrote SK steps ago
+                        above = out_hist[t - SK][:, w - 1] if t >= SK else np.zeros((4, M, 64, 2), np.int64)
                     REC = np.empty((4, M, 64, 2), np.int64)
                     REC[..., 0] = above[..., 1]
                     REC[..., 1] = own_prev[:, w][..., 0]
@@ -171,7 +178,7 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, cel
                     if L == G - 1 and q == GZ - 1:
                         rf = (lb - 1) - L * RW
                         kf = (lc - 1) - q * ZT
-                        if rf // 2 == w and t == (la - 1) + rf + kf:
+                        if rf // 2 == w and t == (la - 1) + tau(rf) + kf:
                             score = int(best[kf % M, kf // M, rf % 2])
                     # ---- z staging: lane 63, register M-1
                     zstep[w] = (oIz[M - 1, 63].copy(), oIxz[M - 1, 63].copy(),
@@ -198,6 +205,7 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, cel
                     svIyz[w] = zshift(REC[2], fz[2])
                     svM[PH, w] = zshift(REC[3], fz[3])
                 out_prev = out_now
+                out_hist.append(out_now)
                 ys.append(out_now[:, NW - 1].copy())
                 zs.append(zstep)
             yrec[(L, q)] = ys
