@@ -8,30 +8,39 @@
 // of the 8x8 PE array's passes and HBM rings in place of the face SRAMs.
 //
 // Inside a workgroup (tools/lap_emu.py replays this schedule on the CPU):
-//  * wave w holds TWO DP rows, y = L*RW + 2w + 1 in the low 16-bit half and
-//    y + 1 in the high half of every packed register -- a lap of RW rows needs
-//    only NW waves, one per SIMD for NW = 4, which is what a latency-bound
-//    chain wants (a step is one wave's dependent instruction stream, not four
-//    waves sharing a SIMD);
+//  * NW compute waves; wave w holds TWO DP rows, y = L*RW + 2w + 1 in the low
+//    16-bit half and y + 1 in the high half of every packed register;
 //  * lane l, register i is tile position k = M*l + i (z = q*ZT + k + 1); half
 //    h of wave w computes x = t - (2w + h) - k + 1 at local step t;
 //  * the high half's row above is the wave's own low half one step earlier, the
-//    low half's is wave w-1's high half (LDS record, one barrier per step):
-//    one v_alignbit/v_perm per record word (REC = {above.hi, own_prev.lo});
+//    low half's is wave w-1's high half of step t-1: one v_alignbit/v_perm per
+//    record word (REC = {above.hi, own_prev.lo});
 //  * z-1 neighbours shift one position per step (register rename, one DPP
 //    wave_ror + one v_perm per message), the x = 1 position takes the x = 0
 //    face (src/PE_1cyc.v:164-218 EN_i gating), as in the helix kernel.
+// No workgroup barrier per step: the waves are a pipeline, each running its
+// own loop and synchronised point to point through LDS (a systolic array of
+// waves, as the RTL's PEs are one of registers):
+//  * wave w writes its record of step t into an LDS ring of K slots and then
+//    its progress word (t + 1); wave w+1 polls that word before reading, and
+//    wave w polls wave w+1's before reusing a slot. A step costs one wave's
+//    own instruction stream; the hand-off latency is paid once per wave, not
+//    once per step (a barrier makes every step pay it);
+//  * wave NW is the LOADER: it LDS-DMAs the records of the lap above (y) and of
+//    the tile to the left (z) LPD steps ahead, checks their tags, re-fetches
+//    stale ones and publishes its own progress word, which wave 0 polls -- the
+//    global hand-off's latency and checks are off the compute waves' path.
 // Between workgroups (MI355X_MICROARCH.md "handoff-1to1"):
-//  * the last wave stores its per-step record (the high halves the next lap's
-//    wave 0 needs) into a y ring of YR slots, and every wave's last position
-//    ({Iz, Ixz, REC.z, REC.w}) goes into a z ring of ZR slots for tile q+1;
+//  * the last compute wave stores its per-step record (the high halves the
+//    next lap's wave 0 needs) into a y ring of YR slots, and every wave's
+//    lane 63 its last position ({Iz, Ixz, REC.z, REC.w}) into a z ring of ZR
+//    slots for tile q+1;
 //  * every 8-byte granule of a record carries a 32-bit tag of (launch epoch,
-//    step), written by one sc1 store: the consumer LDS-DMAs records LPD steps
-//    ahead and checks the tags where it uses them -- no flags, no polls on the
-//    fast path; a stale tag re-fetches (bounded; on timeout the launch's error
-//    word is set and the triple reports TSA_SCORE_INVALID);
-//  * the rings are O(N^2) (O(N) per workgroup): a consumer publishes its
-//    progress every 4 steps and a producer about to overwrite a slot the
+//    step), written by one sc1 store; the loader checks the tags (no flags on
+//    the fast path); a stale tag re-fetches (bounded; on timeout the launch's
+//    error word is set and the triple reports TSA_SCORE_INVALID);
+//  * the rings are O(N^2) (O(N) per workgroup): a consumer publishes how far
+//    its loader has checked, and a producer about to overwrite a slot the
 //    consumer may still need waits for it (never on the fast path: the rings
 //    hold 2-4x the natural lag);
 //  * block b -> XCD b % 8 (observed dispatch, speed only): every lap of a z-tile
@@ -51,32 +60,27 @@
 
 namespace tsa {
 
-#ifndef TSA_LAP_PD1  // LDS-DMA prefetch distance (steps) by M: build-time knobs
-#define TSA_LAP_PD1 3
-#endif
+#ifndef TSA_LAP_PD1  // loader prefetch distance (steps) by M: build-time knobs. Short
+#define TSA_LAP_PD1 2  // wins: a fetch issued before its producer stored is a tag miss
+#endif                 // and a serial re-fetch (A/B on MI355X: 2 < 3 < 4 < 6)
 #ifndef TSA_LAP_PD2
-#define TSA_LAP_PD2 6
+#define TSA_LAP_PD2 2
 #endif
 #ifndef TSA_LAP_PD4
-#define TSA_LAP_PD4 4
+#define TSA_LAP_PD4 3
 #endif
 __host__ __device__ constexpr int lap_pd(int M) {
   return M == 1 ? TSA_LAP_PD1 : M == 2 ? TSA_LAP_PD2 : TSA_LAP_PD4;
 }
-constexpr int LAP_ZL = 16;         // z records resident in LDS (power of 2, > lap_pd + 2)
-constexpr int LAP_PUB = 4;         // consumers publish their progress every LAP_PUB steps
+// LDS ring slots: wave -> wave (K) and loader -> wave 0 (K0); powers of 2
+__host__ __device__ constexpr int lap_k(int M) { return M == 1 ? 4 : 2; }
+__host__ __device__ constexpr int lap_k0(int M) { return M <= 2 ? 8 : 4; }
+constexpr int LAP_ZL = 32;           // z records resident in LDS (power of 2)
+constexpr int LAP_PUB = 4;           // the last wave publishes the consumer progress every LAP_PUB steps
 constexpr int LAP_PROG_STRIDE = 32;  // progress words 128 B apart (one line each)
-constexpr int LAP_ZREC_WAVE = 32;  // z record bytes per wave: 4 x {payload, tag}
+constexpr int LAP_ZREC_WAVE = 32;    // z record bytes per wave: 2 x {payload, tag, payload, tag}
 
-#ifndef TSA_LAP_SKEW  // steps between a wave's high row and the next wave's low row
-#define TSA_LAP_SKEW 1
-#endif
-// SK = 1: one barrier per step, the wave below reads this step's record next
-// step; SK = 2: a wave reads the record of two steps ago, one barrier per two
-// steps (tools/lap_emu.py replays both)
-constexpr int LAP_SK = TSA_LAP_SKEW;
-static_assert(LAP_SK == 1 || LAP_SK == 2, "lap skew");
-static_assert(LAP_ZL > TSA_LAP_PD1 + 2 + LAP_SK && LAP_ZL > TSA_LAP_PD2 + 2 + LAP_SK, "z slots");
+static_assert(LAP_ZL >= 8 + 2 + TSA_LAP_PD1 + 2 && LAP_ZL >= 8 + 2 + TSA_LAP_PD2 + 2, "z slots");
 
 // Tag of the record of step s in the launch with epoch e (32-bit): distinct
 // steps of one launch never collide (odd multiplier).
@@ -86,10 +90,19 @@ __host__ __device__ __forceinline__ uint32_t lap_tag(uint32_t e, int32_t s) {
 
 static size_t lap_lds_bytes(int M, int NW, int32_t max_la) {
   const int ZT = 64 * M, SLOT = M * 1024;
-  return (size_t)(NW - 1) * 2 * LAP_SK * SLOT + (size_t)lap_pd(M) * SLOT + 4 * (size_t)NW * 16 +
-         (size_t)LAP_ZL * NW * LAP_ZREC_WAVE + 16 + (size_t)M * 256 +
-         4 * (((size_t)max_la + 2 * ZT + 2 * (LAP_SK + 1) * NW + 8 + 3) & ~(size_t)3);
+  return (size_t)(NW - 1) * lap_k(M) * SLOT + (size_t)lap_k0(M) * SLOT +
+         (size_t)LAP_ZL * NW * LAP_ZREC_WAVE + (size_t)SLOT + (size_t)NW * LAP_ZREC_WAVE + 16 * 4 +
+         (size_t)(NW + 1) * 256 + (size_t)M * 256 +
+         4 * (((size_t)max_la + 2 * ZT + 4 * NW + 8 + 3) & ~(size_t)3);
 }
+
+// Trace slots per block (TSA_LAP_TRACE): 8, plus with TSA_LAP_PROF (a
+// diagnostic build) 4 shader-clock accumulators per compute wave.
+#if defined(TSA_LAP_PROF)
+constexpr int LAP_TRACE_SLOTS = 8 + 4 * 8;
+#else
+constexpr int LAP_TRACE_SLOTS = 8;
+#endif
 
 // ---------------------------------------------------------------------------
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -119,20 +132,178 @@ __device__ __forceinline__ int32_t lds_word(const int32_t *p) {
       *(volatile const __attribute__((address_space(3))) int32_t *)(
           const __attribute__((address_space(3))) void *)p);
 }
+// Progress word store: every lane writes its own copy (pw[wave][lane], one
+// conflict-free ds_write_b32, no exec toggling); readers read lane 0's. LDS
+// executes a wave's DS instructions in order, so a reader that sees the word
+// also sees the record written before it; the empty asm keeps the compiler
+// from moving LDS accesses across it.
+__device__ __forceinline__ void lds_publish(int32_t *pw_wave, int32_t v, int lane) {
+  asm volatile("" ::: "memory");
+#if defined(TSA_LAP_LDS_FENCE)  // A/B knob: drain this wave's LDS writes first
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+  *(volatile __attribute__((address_space(3))) int32_t *)(__attribute__((address_space(3))) void *)(
+      pw_wave + lane) = v;
+  asm volatile("" ::: "memory");
+}
+// Lane bit `k` of a 64-bit exec-style mask when 0 <= k < 64, else 0 -- in SALU
+// (left to itself the compiler shifts a 64-bit 1 in VALU and reads it back).
+__device__ __forceinline__ uint64_t lane_bit(int32_t k) {
+  uint64_t r;
+  asm("s_lshl_b64 %0, 1, %1\n\ts_cmp_lt_u32 %1, 64\n\ts_cselect_b64 %0, %0, 0"
+      : "=&s"(r) : "s"(k) : "scc");
+  return r;
+}
+
+// The lap kernel's cell, split at the row above (the message form of
+// cell_messages_f16 / cell_messages, src/PE_1cyc.v:159-218): of a step's
+// inputs only Iy comes from this step's record -- x-1, z-1, the diagonals and
+// the scores are known when the step starts -- so every message is folded to
+// max(Y - c, N) with the N's computed while the record is read. GO >= GE
+// orders the penalties (E <= O, 2E <= O+E <= 2O, f16 form with the mismatch
+// folded into E and O alike), so Y's dominated copies drop out:
+//   best = max(Y, W),       W  = max(X, Z, XY, XZ, YZ, M)
+//   Ix'  = max(Y - OE, N1), N1 = max(X - 2E, U1 - OE, W - 2O), U1 = max(X, Z, XY, XZ)
+//   Iy'  = max(Y - 2E, N2), N2 = max(U2 - OE, W - 2O),         U2 = max(X, Z, XY, YZ)
+//   Iz'  = max(Y - OE, N3), N3 = max(Z - 2E, U3 - OE, W - 2O), U3 = max(X, Z, XZ, YZ)
+//   Ixy' = max(Y - E, N4),  N4 = max(max(X, XY) - E, W - O)
+//   Iyz' = max(Y - E, N5),  N5 = max(max(YZ, Z) - E, W - O)
+//   Ixz' = max(Y - O, N6),  N6 = max(max(X, Z, XZ) - E, W - O)
+// (11 dependent instructions per pair after the record lands instead of ~30).
+template <int M>
+struct LapPre {
+  uint32_t W[M], N1[M], N2[M], N3[M], N4[M], N5[M], N6[M];
+};
+template <int M, bool SOP>
+__device__ __forceinline__ void lap_pre_f16(const uint32_t (&a)[M], const uint32_t (&b)[M],
+                                            const uint32_t (&c)[M], const uint32_t (&SBC)[M],
+                                            const uint32_t (&K)[M], const uint32_t (&DMC)[M],
+                                            uint32_t Q, const PencilArgs &pa,
+                                            const uint32_t (&inIx)[M], const uint32_t (&inIz)[M],
+                                            const uint32_t (&inIxy)[M], const uint32_t (&inIyz)[M],
+                                            const uint32_t (&inIxz)[M], const uint32_t (&inM)[M],
+                                            LapPre<M> &p) {
+  const h2 DM = H(pa.h_dm), E = H(pa.E), O = H(pa.O), E2 = H(pa.E2), OE = H(pa.OE), O2 = H(pa.O2);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const h2 eab = H(umin2(a[i] & b[i], Q)), eac = H(a[i] & c[i]), DMCi = H(DMC[i]);
+    const h2 sXY = hfma(eab, DM, H(inIxy[i]));  // src/PE_1cyc.v:159-161 (+mismatch folded)
+    const h2 sXZ = hfma(eac, DMCi, H(inIxz[i]));
+    const h2 sYZ = H(inIyz[i]) + H(SBC[i]);
+    h2 sM;                                       // src/PE_1cyc.v:162
+    if constexpr (SOP) sM = hfma(eab, DM, hfma(eac, DMCi, H(inM[i]))) + H(K[i]);
+    else sM = hfma(eab, H(K[i]), H(inM[i])) + H(pa.h_c3);
+    const h2 X = H(inIx[i]), Z = H(inIz[i]);
+    const h2 pXZ = hmax(X, Z);
+    const h2 U1 = vmax3(pXZ, sXY, sXZ), U2 = vmax3(pXZ, sXY, sYZ), U3 = vmax3(pXZ, sYZ, sXZ);
+    const h2 W = vmax3(U1, sYZ, sM);
+    const h2 WO = W - O, WO2 = W - O2;
+    p.W[i] = U(W);
+    p.N1[i] = U(vmax3(X - E2, U1 - OE, WO2));
+    p.N2[i] = U(hmax(U2 - OE, WO2));
+    p.N3[i] = U(vmax3(Z - E2, U3 - OE, WO2));
+    p.N4[i] = U(hmax(hmax(X, sXY) - E, WO));
+    p.N5[i] = U(hmax(hmax(sYZ, Z) - E, WO));
+    p.N6[i] = U(hmax(hmax(pXZ, sXZ) - E, WO));
+  }
+}
+template <int M>
+__device__ __forceinline__ void lap_post_f16(const PencilArgs &pa, const uint32_t (&Y)[M],
+                                             const LapPre<M> &p, uint32_t (&nIx)[M],
+                                             uint32_t (&oIy)[M], uint32_t (&oIz)[M],
+                                             uint32_t (&oIxy)[M], uint32_t (&oIyz)[M],
+                                             uint32_t (&oIxz)[M], uint32_t (&oBest)[M]) {
+  const h2 E = H(pa.E), O = H(pa.O), E2 = H(pa.E2), OE = H(pa.OE);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const h2 y = H(Y[i]), yOE = y - OE, yE = y - E;
+    oBest[i] = U(hmax(y, H(p.W[i])));
+    nIx[i] = U(hmax(yOE, H(p.N1[i])));
+    oIy[i] = U(hmax(y - E2, H(p.N2[i])));
+    oIz[i] = U(hmax(yOE, H(p.N3[i])));
+    oIxy[i] = U(hmax(yE, H(p.N4[i])));
+    oIyz[i] = U(hmax(yE, H(p.N5[i])));
+    oIxz[i] = U(hmax(y - O, H(p.N6[i])));
+  }
+}
+// int16 form (two's complement halves): the same split of cell_messages
+template <int M, bool SOP>
+__device__ __forceinline__ void lap_pre_i16(const uint32_t (&a)[M], const uint32_t (&b)[M],
+                                            const uint32_t (&c)[M], uint32_t ones,
+                                            const PencilArgs &pa, const uint32_t (&inIx)[M],
+                                            const uint32_t (&inIz)[M], const uint32_t (&inIxy)[M],
+                                            const uint32_t (&inIyz)[M], const uint32_t (&inIxz)[M],
+                                            const uint32_t (&inM)[M], LapPre<M> &p) {
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const uint32_t eab = pk_eq1(a[i], b[i], ones);
+    const uint32_t eac = pk_eq1(a[i], c[i], ones);
+    const uint32_t ebc = pk_eq1(b[i], c[i], ones);
+    const uint32_t s2ab = pk_mad(eab, pa.dm, pa.mm);
+    const uint32_t s2ac = pk_mad(eac, pa.dm, pa.mm);
+    const uint32_t s2bc = pk_mad(ebc, pa.dm, pa.mm);
+    uint32_t s3;
+    if constexpr (SOP) s3 = pk_add(pk_add(s2ab, s2bc), s2ac);
+    else s3 = pk_mad(eab, pk_mad(ebc, pa.s3_d1, pa.s3_d0), pa.s3_ne);
+    const uint32_t sM = pk_add(inM[i], s3), X = inIx[i], Z = inIz[i];
+    const uint32_t sXY = pk_add(inIxy[i], s2ab), sYZ = pk_add(inIyz[i], s2bc);
+    const uint32_t sXZ = pk_add(inIxz[i], s2ac);
+    const uint32_t pXZ = pk_max(X, Z);
+    const uint32_t U1 = pk_max(pk_max(pXZ, sXY), sXZ), U2 = pk_max(pk_max(pXZ, sXY), sYZ);
+    const uint32_t U3 = pk_max(pk_max(pXZ, sYZ), sXZ), W = pk_max(pk_max(U1, sYZ), sM);
+    const uint32_t WO = pk_sub(W, pa.O), WO2 = pk_sub(W, pa.O2);
+    p.W[i] = W;
+    p.N1[i] = pk_max(pk_max(pk_sub(X, pa.E2), pk_sub(U1, pa.OE)), WO2);
+    p.N2[i] = pk_max(pk_sub(U2, pa.OE), WO2);
+    p.N3[i] = pk_max(pk_max(pk_sub(Z, pa.E2), pk_sub(U3, pa.OE)), WO2);
+    p.N4[i] = pk_max(pk_sub(pk_max(X, sXY), pa.E), WO);
+    p.N5[i] = pk_max(pk_sub(pk_max(sYZ, Z), pa.E), WO);
+    p.N6[i] = pk_max(pk_sub(pk_max(pXZ, sXZ), pa.E), WO);
+  }
+}
+template <int M>
+__device__ __forceinline__ void lap_post_i16(const PencilArgs &pa, const uint32_t (&Y)[M],
+                                             const LapPre<M> &p, uint32_t (&nIx)[M],
+                                             uint32_t (&oIy)[M], uint32_t (&oIz)[M],
+                                             uint32_t (&oIxy)[M], uint32_t (&oIyz)[M],
+                                             uint32_t (&oIxz)[M], uint32_t (&oBest)[M]) {
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const uint32_t y = Y[i], yOE = pk_sub(y, pa.OE), yE = pk_sub(y, pa.E);
+    oBest[i] = pk_max(y, p.W[i]);
+    nIx[i] = pk_max(yOE, p.N1[i]);
+    oIy[i] = pk_max(pk_sub(y, pa.E2), p.N2[i]);
+    oIz[i] = pk_max(yOE, p.N3[i]);
+    oIxy[i] = pk_max(yE, p.N4[i]);
+    oIyz[i] = pk_max(yE, p.N5[i]);
+    oIxz[i] = pk_max(pk_sub(y, pa.O), p.N6[i]);
+  }
+}
 
 // LDS (bytes):
-//   xr    [NW-1][2SK][M][64][16] wave w -> w+1 records {Iy, Ixy, Iyz, best}
-//   xr0   [LPD][M][64][16]      tagged y records of the lap above (LDS-DMA)
-//   zst   [4][NW][16]           z staging {Iz, Ixz, REC.z, REC.w} of lane 63
-//   zring [ZL][NW][32]          tagged z records of the tile to the left
-//   bpw   [4] i32               consumers' progress words (LDS-DMA'd)
+//   xr    [NW-1][K][M][64][16]  wave w -> w+1 records {Iy, Ixy, Iyz, best}
+//   xr0   [K0][M][64][16]       tagged y records of the lap above (loader, LDS-DMA)
+//   zring [ZL][NW][32]          tagged z records of the tile to the left (loader)
+//   yface [M][64][16]           y = 0 face in wave 0's record format (lap 0)
+//   zface [NW][32]              z = 0 face in the z record format (tile 0)
+//   wd    [16] i32              [9] back-pressure waits, [12] abort, [13..14] the
+//                               consumers' progress (LDS-DMA'd), [15] loader stalls
+//   pw    [NW+1][64] i32        progress words (steps done): compute wave w, loader NW
 //   fin   [M][64] u32           best of the final step
 //   sA2   [..] u32              A code pairs: entry j = x j-OFF (lo), j-OFF-1 (hi)
 // Minimum waves per SIMD the register allocation must allow: pins occupancy
 // (and keeps SGPRs <= ~80, which the CU's admission of 256-thread blocks also
 // depends on, MI355X_MICROARCH.md "Residency"), so the occupancy API's answer
 // is what the hardware admits and a resident grid stays resident.
-__host__ __device__ constexpr int lap_waves_per_eu(int M) { return M == 1 ? 8 : M == 2 ? 4 : 2; }
+__host__ __device__ constexpr int lap_waves_per_eu(int M) { return M == 1 ? 4 : M == 2 ? 5 : 2; }
+// f(integral_constant<J>) for J = B .. E-1, unrolled at compile time
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
 // every step of the lap kernel inlined (outlined, the captures go to scratch)
 #define LAP_INLINE(call) \
   do {                    \
@@ -140,29 +311,33 @@ __host__ __device__ constexpr int lap_waves_per_eu(int M) { return M == 1 ? 8 : 
   } while (0)
 
 template <int M, int NW, bool F16, bool SOP>
-__global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
+__global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel(
     const uint8_t *__restrict__ seqs, const int64_t *__restrict__ offs, int32_t G, int32_t GZ,
     int32_t NC, int32_t CH, int32_t YR, int32_t ZR, uint8_t *__restrict__ yf_base,
     uint8_t *__restrict__ zf_base, int32_t *__restrict__ prog, uint32_t *__restrict__ err,
     int32_t *__restrict__ scores, PencilArgs pa, uint32_t epoch, uint32_t spin_limit,
     unsigned long long *__restrict__ trace) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  constexpr int RW = 2 * NW, ZT = 64 * M, LPD = lap_pd(M);
+  constexpr int RW = 2 * NW, ZT = 64 * M, LPD = lap_pd(M), K = lap_k(M), K0 = lap_k0(M);
   constexpr int PAIR = 64 * REC_BYTES, SLOT = M * PAIR;
-  // wave w's rows sit at step offsets WO*w (low half) and WO*w + 1 (high);
-  // lap L+1 reads lap L's record t + YOFF; z records are checked ZV steps ahead
-  constexpr int SK = LAP_SK, WO = SK + 1, NSL = 2 * SK, YOFF = WO * (NW - 1) + 1, ZV = SK;
-  constexpr int ZREC = NW * LAP_ZREC_WAVE, OFF = ZT + WO * NW;
+  // wave w's rows sit at step offsets 2w (low half) and 2w + 1 (high); lap L+1
+  // reads lap L's record t + YOFF; loader step s checks y record s + YOFF and
+  // z record s + ZT + ZA (ZA = NW: every wave's z reads stay covered)
+  constexpr int YOFF = 2 * (NW - 1) + 1, ZA = NW;
+  constexpr int ZREC = NW * LAP_ZREC_WAVE, OFF = ZT + 2 * NW;
   uint8_t *xr = smem;
-  uint8_t *xr0 = xr + (NW - 1) * NSL * SLOT;
-  uint8_t *zst = xr0 + LPD * SLOT;
-  uint8_t *zring = zst + 4 * NW * 16;
-  int32_t *bpw = (int32_t *)(zring + LAP_ZL * ZREC);
-  uint32_t *fin = (uint32_t *)(bpw + 4);
+  uint8_t *xr0 = xr + (NW - 1) * K * SLOT;
+  uint8_t *zring = xr0 + K0 * SLOT;
+  uint8_t *yface = zring + LAP_ZL * ZREC;
+  uint8_t *zface = yface + SLOT;
+  int32_t *wd = (int32_t *)(zface + ZREC);
+  int32_t *pw = wd + 16;
+  uint32_t *fin = (uint32_t *)(pw + 64 * (NW + 1));
   uint32_t *sA2 = fin + M * 64;
+  int32_t *const w_bp = wd + 9, *const w_abort = wd + 12, *const bpw = wd + 13, *const w_stall = wd + 15;
 
   const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // w == NW: the loader
   // block -> (lap, column): column c = tri*GZ + q (one z-tile of one triple), block
   // b = 8 * (L*CH + c/8) + c%8 -- a column's laps share b % 8 (one XCD), and
   // every producer ((L-1, c), (L, c-1)) has a lower block index than its consumer
@@ -176,7 +351,7 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
   const int32_t nlap = (lb + RW - 1) / RW, ntile = (lc + ZT - 1) / ZT;
   if (L >= nlap || q >= ntile) return;  // beyond this triple's own laps / tiles
   auto stamp = [&](int s, unsigned long long v) {
-    if (trace != nullptr && threadIdx.x == 0) trace[(int64_t)b * 8 + s] = v;
+    if (trace != nullptr && threadIdx.x == 0) trace[(int64_t)b * LAP_TRACE_SLOTS + s] = v;
   };
   auto now = [&]() {
     unsigned long long v;
@@ -193,7 +368,7 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
   const bool yin = L > 0, zin = q > 0, yout = L + 1 < nlap, zout = q + 1 < ntile;
   const int32_t zt_q = min(ZT, lc - q * ZT), rows = min(RW, lb - L * RW);
   const bool final_wg = !yout && !zout;
-  auto tau = [](int32_t r) { return WO * (r >> 1) + (r & 1); };  // step offset of lap row r
+  auto tau = [](int32_t r) { return 2 * (r >> 1) + (r & 1); };  // step offset of lap row r
   const int32_t r_f = lb - 1 - L * RW, k_f = lc - 1 - q * ZT;
   const int32_t T = final_wg ? (la - 1) + tau(r_f) + k_f + 1 : la + tau(rows - 1) + zt_q - 1;
   const int32_t T_above = la + tau(RW - 1) + zt_q - 1;  // records the lap above writes (same tile)
@@ -204,388 +379,519 @@ __global__ __launch_bounds__(64 * NW, lap_waves_per_eu(M)) void lap_kernel(
   const uint8_t *zf_prev = zin ? zf_base + (lid - 1) * ZR * ZREC : zf_mine;
   const uint32_t ep19 = epoch & 0x7FFFFu;
   bool timed_out = false;
-  auto fail = [&]() {  // release: visible before any record this workgroup stores later
-    if (!timed_out && lane == 0)
+  auto fail = [&]() {  // every wait of this workgroup gives up from now on
+    if (!timed_out && lane == 0) {
       __hip_atomic_store(err, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      *(volatile __attribute__((address_space(3))) int32_t *)(__attribute__((address_space(3))) void *)w_abort = 1;
+    }
     timed_out = true;
   };
+  // wait until an LDS progress word reaches `need` (bounded: a hand-off timeout
+  // upstream aborts the workgroup, and no wait outlives ~4 x spin_limit polls)
+  uint32_t n_wait = 0;
+  auto wait_word = [&](const int32_t *word, int32_t &seen, int32_t need) {
+    if (need <= seen) return;
+    seen = lds_word(word);
+    if (need <= seen) return;
+    ++n_wait;
+    for (uint32_t spin = 1;; ++spin) {
+      seen = lds_word(word);
+      if (need <= seen) return;
+      if ((spin & 255) == 0 && (timed_out || lds_word(w_abort) != 0 || spin >= 4 * spin_limit)) {
+        fail();
+        seen = 1 << 24;
+        return;
+      }
+      if (spin > 64) __builtin_amdgcn_s_sleep(1);
+    }
+  };
 
-  // ---- A code pairs, per-row and per-position registers
-  const int32_t na = la + 2 * ZT + 2 * WO * NW + 8;
-  for (int j = threadIdx.x; j < na; j += 64 * NW) {
+  // ---- A code pairs, zeroed words
+  const int32_t na = la + 2 * ZT + 4 * NW + 8;
+  for (int j = threadIdx.x; j < na; j += 64 * (NW + 1)) {
     const int x0 = j - OFF, x1 = j - OFF - 1;
     const uint32_t c0 = (x0 >= 0 && x0 < la) ? SYM0 << (seqs[o0 + x0] & 3) : 0u;
     const uint32_t c1 = (x1 >= 0 && x1 < la) ? SYM0 << (seqs[o0 + x1] & 3) : 0u;
     sA2[j] = c0 | (c1 << 16);
   }
-  // a[i] of this lane at step t = sA2[t - WO w - (M lane + i) + OFF]
-  const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
-                          4u * (uint32_t)(OFF - WO * w - M * lane - (M - 1));
-  const int32_t y0 = L * RW + 2 * w;  // rows y0 (lo) and y0 + 1 (hi), 0-based
-  const uint32_t bw = (y0 < lb ? SYM0 << (seqs[o1 + y0] & 3) : 0u) |
-                      ((y0 + 1 < lb ? SYM0 << (seqs[o1 + y0 + 1] & 3) : 0u) << 16);
-  uint32_t bv[M], c[M], SBC[M], K[M], DMC[M];
-  uint32_t oIx[M], shIz[M], svIxy[M], svIyz[M], shIxz[2][M], svM[2][M];
-  uint32_t pIy[M], pIxy[M], pIyz[M], pBest[M];  // this wave's record of the previous step
-  {
-    uint32_t one1 = 0x00010001u, sbcv = pa.h_sbc, kdv = pa.h_kd, k0v = pa.h_k0;
-    asm volatile("" : "+v"(one1), "+v"(sbcv), "+v"(kdv), "+v"(k0v));
-    const int64_t oc = o2 + (int64_t)q * ZT;
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      const int k = M * lane + i;
-      c[i] = (k < zt_q ? SYM0 << (seqs[oc + k] & 3) : 0u) * 0x00010001u;
-      DMC[i] = dm_over_code(pa.dmf, c[i]);
-      bv[i] = bw;
-      const uint32_t e01 = pk_eq1(bw, c[i], one1);
-      SBC[i] = pk_mad(e01, sbcv, 0u);
-      K[i] = pk_mad(e01, kdv, k0v);
-      oIx[i] = shIz[i] = pa.f_single;
-      shIxz[0][i] = shIxz[1][i] = svIxy[i] = svIyz[i] = pa.f_pair;
-      svM[0][i] = svM[1][i] = 0;
-      pIy[i] = pIxy[i] = pIyz[i] = pBest[i] = 0;
-    }
-  }
-  uint32_t Q = F16 ? 0x08000800u : 0x00010001u, fsv = pa.f_single, fpv = pa.f_pair;
-  uint32_t mlo = 0x0000FFFFu, mhi = 0xFFFF0000u;
-  asm volatile("" : "+v"(Q), "+v"(fsv), "+v"(fpv), "+v"(mlo), "+v"(mhi));
-  const PencilArgs pv = F16 ? pa : pin_score_consts(pa);
-  const uint32_t sel0 = lane == 0 ? 0x03020100u : 0x07060504u;  // lane 0: whole word from the face
-
-  // ---- producer side (last wave): the consumers' progress (y: lap below, z: tile right)
-  const int64_t cons_y = yout ? lid + GZ : -1, cons_z = zout ? lid + 1 : -1;
-  int32_t seen_y = -1, seen_z = -1;  // consumer steps known to be complete
-  auto prog_decode = [&](int32_t v) -> int32_t {
-    return ((uint32_t)v >> 13) == ep19 ? (int32_t)(v & 0x1FFF) - 1 : -1;
-  };
-  uint32_t n_stall = 0, n_bp = 0;  // diagnostics (trace)
-  // wait until the consumer's progress covers `need`; the LDS word is a lower
-  // bound refreshed by LDS-DMA every 8 steps, the blocking poll the slow path
-  auto wait_consumer = [&](int64_t cons, int32_t &seen, int32_t *word, int32_t need) {
-    if (need <= seen) return;
-    seen = max(seen, prog_decode(lds_word(word)));
-    if (need <= seen) return;
-    ++n_bp;
-    for (uint32_t spin = 0;; ++spin) {
-      const int32_t v = __builtin_amdgcn_readfirstlane(
-          __hip_atomic_load(prog + cons * LAP_PROG_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      seen = max(seen, prog_decode(v));
-      if (need <= seen) return;
-      if (spin >= spin_limit) { fail(); seen = 1 << 20; return; }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  };
-
-  // ---- consumer side (wave 0): fetches, tag checks
-  auto fetch_y = [&](int32_t s) {  // records of step s (row s + YOFF above) -> xr0 slot s % LPD
-    const int32_t r = s + YOFF;
-#pragma unroll
-    for (int i = 0; i < M; ++i)
-      dma16(yf_prev + ((int64_t)(r & (YR - 1)) * M + i) * PAIR + lane * REC_BYTES,
-            xr0 + (s % LPD) * SLOT + i * PAIR);
-  };
-  auto fetch_z = [&](int32_t rz) {  // z record rz -> zring slot rz % ZL (lanes 0 .. 2NW-1)
-    if (lane < 2 * NW)
-      dma16(zf_prev + (int64_t)(rz & (ZR - 1)) * ZREC + lane * 16,
-            zring + (rz & (LAP_ZL - 1)) * ZREC);
-  };
-  auto y_ok = [&](const uint4 (&rv)[M], int32_t r) {
-    const uint32_t tg = lap_tag(epoch, r);
-    bool ok = true;
-#pragma unroll
-    for (int i = 0; i < M; ++i) ok = ok && rv[i].y == tg && rv[i].w == tg;
-    return __all(ok) != 0;
-  };
-  auto z_ok = [&](int32_t rz) {
-    const uint32_t tg = lap_tag(epoch, rz);
-    bool ok = true;
-    if (lane < 2 * NW) {
-      const uint4 v = lds_read16(zring + (rz & (LAP_ZL - 1)) * ZREC + lane * 16);
-      ok = v.y == tg && v.w == tg;
-    }
-    return __all(ok) != 0;
-  };
-  // slow path: re-fetch until the tags match (the producer has not stored yet)
-  auto settle_z = [&](int32_t rz) {
-    if (!zin || rz >= T_left) return;
-    if (z_ok(rz)) return;
-    ++n_stall;
-    for (uint32_t spin = 0;; ++spin) {
-      if (spin >= spin_limit) { fail(); return; }
-      __builtin_amdgcn_s_sleep(1);
-      fetch_z(rz);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (z_ok(rz)) return;
-    }
-  };
-
-  // prologue (wave 0): z records ZT-2 and ZT-1 (what the shifts of steps -2 and
-  // -1 would have brought into position 0: its Iz/Iyz inputs of step 0 and its
-  // Ixz/M inputs of steps 0 and 1) and ZT .. ZT+ZV-1 (the shifts before the
-  // first check); then LPD steps of y and z fetches -- M + 1 DMAs per step,
-  // always (dummy ones where there is no producer), so the per-step vmcnt count
-  // is a constant
-  if (w == 0) {
-    if (lane < 4) bpw[lane] = 0;
-    if (zin) {
-      for (int rz = ZT - 2; rz < ZT + ZV; ++rz) fetch_z(rz);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      for (int rz = ZT - 2; rz < ZT + ZV; ++rz) settle_z(rz);
-    }
-    for (int s = 0; s < LPD; ++s) {
-      fetch_y(s);
-      fetch_z(s + ZT + ZV);
-    }
-  }
+  if (threadIdx.x < 16) wd[threadIdx.x] = 0;
+  // face records, so a lap-0 wave 0 / tile-0 wave reads its y / z inputs the
+  // same way as any other (no branch in the step): y {Iy, Ixy | Iyz, best} low
+  // halves (wave 0's perm format), z {Iz, -, Ixz, - | Iyz, -, M, -}
+  for (int j = threadIdx.x; j < M * 64; j += 64 * (NW + 1))
+    ((uint4 *)yface)[j] = make_uint4((pa.f_single & 0xFFFFu) | (pa.f_pair & 0xFFFF0000u), 0u,
+                                     pa.f_pair & 0xFFFFu, 0u);
+  if (threadIdx.x < 2 * NW)
+    ((uint4 *)zface)[threadIdx.x] = (threadIdx.x & 1) ? make_uint4(pa.f_pair, 0u, 0u, 0u)
+                                                      : make_uint4(pa.f_single, 0u, pa.f_pair, 0u);
+  pw[threadIdx.x] = 0;  // blockDim = 64 (NW + 1): one word per thread
   __syncthreads();
-  if (zin) {  // position 0 before step 0 (tools/lap_emu.py: the same initial shifts)
-    const uint8_t *r1 = zring + ((ZT - 1) & (LAP_ZL - 1)) * ZREC + w * LAP_ZREC_WAVE;
-    const uint8_t *r2 = zring + ((ZT - 2) & (LAP_ZL - 1)) * ZREC + w * LAP_ZREC_WAVE;
-    const uint4 a0 = lds_read16(r1), a1 = lds_read16(r1 + 16);
-    const uint4 b0 = lds_read16(r2), b1 = lds_read16(r2 + 16);
-    if (lane == 0) {
-      shIz[0] = a0.x;
-      svIyz[0] = a1.x;
-      shIxz[1][0] = a0.z;
-      svM[1][0] = a1.z;
-      shIxz[0][0] = b0.z;
-      svM[0][0] = b1.z;
-    }
-  }
-  if (trace != nullptr) stamp(1, now());
-  const uint4 face = make_uint4(pa.f_single, pa.f_pair, pa.f_pair, 0u);
-  uint32_t a_nx[M];
-  load_a<M>(a_lane, a_nx);
 
-  // ROLE: 0 = wave 0, 1 = middle waves, 2 = the last wave (NW >= 2)
-  auto step = [&](auto ph, auto role, int32_t t, auto fin_step) {
-    constexpr int PH = decltype(ph)::value;
-    constexpr int ROLE = decltype(role)::value;
-    constexpr bool FIN = decltype(fin_step)::value;
-    uint32_t a[M];
+  if (w == NW) {
+    // =================== loader wave ===================
+    // Records are fetched LPD steps ahead into registers with 8-byte sc1 loads
+    // (one {payload, tag} granule each: relaxed agent-scope atomics, so the
+    // compiler counts vmcnt itself), their tags checked in registers, then
+    // written to LDS (xr0 / zring) and published.
+    uint32_t stalls = 0;
+    typedef unsigned long long u64;
+    auto gl8 = [](const uint8_t *p) -> u64 {
+      return __hip_atomic_load((const u64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    const int64_t cons_y = yout ? lid + GZ : lid, cons_z = zout ? lid + 1 : lid;
+    struct Fetch {
+      u64 y[2 * M], z[2];
+      int32_t py, pz;  // my consumers' progress words (lane 0)
+    };
+    auto fetch_y = [&](int32_t s, Fetch &f) {  // y record s + YOFF
+      const int32_t r = s + YOFF;
 #pragma unroll
-    for (int i = 0; i < M; ++i) a[i] = a_nx[i];
-    load_a<M>(a_lane + 4u * (uint32_t)(t + 1), a_nx);  // lands by the step barrier
-    // ---- the row above of both halves
-    uint32_t Ry[M], Rxy[M], Ryz[M], Rb[M];
-    if constexpr (ROLE == 0) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((M + 1) * (LPD - 1)) : "memory");
-      if (yin) {
-        const int32_t r = t + YOFF;
-        uint4 rv[M];
-        const uint8_t *src = xr0 + (t % LPD) * SLOT + lane * REC_BYTES;
+      for (int i = 0; i < M; ++i) {
+        const uint8_t *g = yf_prev + ((int64_t)(r & (YR - 1)) * M + i) * PAIR + lane * REC_BYTES;
+        f.y[2 * i] = gl8(g);
+        f.y[2 * i + 1] = gl8(g + 8);
+      }
+    };
+    auto fetch_z = [&](int32_t rz, Fetch &f) {  // z record rz (lanes 0 .. 2NW-1)
+      const uint8_t *g = zf_prev + (int64_t)(rz & (ZR - 1)) * ZREC + (lane & (2 * NW - 1)) * 16;
+      f.z[0] = gl8(g);
+      f.z[1] = gl8(g + 8);
+    };
+    auto fetch = [&](int32_t s, Fetch &f) {
+      fetch_y(s, f);
+      fetch_z(s + ZT + ZA, f);
+      f.py = __hip_atomic_load(prog + cons_y * LAP_PROG_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      f.pz = __hip_atomic_load(prog + cons_z * LAP_PROG_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto tag_ok = [](u64 g, uint32_t tg) { return (uint32_t)(g >> 32) == tg; };
+    auto y_ok = [&](int32_t s, const Fetch &f) {
+      const uint32_t tg = lap_tag(epoch, s + YOFF);
+      bool ok = true;
 #pragma unroll
-        for (int i = 0; i < M; ++i) rv[i] = lds_read16(src + i * PAIR);
-        if (r < T_above && !y_ok(rv, r)) {
-          ++n_stall;
-          for (uint32_t spin = 0;; ++spin) {
-            if (spin >= spin_limit) { fail(); break; }
-            __builtin_amdgcn_s_sleep(1);
-            fetch_y(t);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int i = 0; i < M; ++i) rv[i] = lds_read16(src + i * PAIR);
-            if (y_ok(rv, r)) break;
-          }
+      for (int i = 0; i < 2 * M; ++i) ok = ok && tag_ok(f.y[i], tg);
+      return __all(ok) != 0;
+    };
+    auto z_ok = [&](int32_t rz, const Fetch &f) {
+      const uint32_t tg = lap_tag(epoch, rz);
+      return __all(lane >= 2 * NW || (tag_ok(f.z[0], tg) && tag_ok(f.z[1], tg))) != 0;
+    };
+    // slow path: fetch again until the tags match (the producer has not stored yet)
+    auto settle_y = [&](int32_t s, Fetch &f) {
+      ++stalls;
+      for (uint32_t spin = 0;; ++spin) {
+        if (spin >= spin_limit || timed_out || ((spin & 63) == 63 && lds_word(w_abort) != 0)) {
+          fail();
+          return;
         }
-        // tagged record {Iy.hi | Ixy.hi << 16, tag, Iyz.hi | best.hi << 16, tag}
+        fetch_y(s, f);
+        if (y_ok(s, f)) return;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    };
+    auto settle_z = [&](int32_t rz, Fetch &f) {
+      ++stalls;
+      for (uint32_t spin = 0;; ++spin) {
+        if (spin >= spin_limit || timed_out || ((spin & 63) == 63 && lds_word(w_abort) != 0)) {
+          fail();
+          return;
+        }
+        fetch_z(rz, f);
+        if (z_ok(rz, f)) return;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    };
+    auto put_z = [&](int32_t rz, const Fetch &f) {
+      if (lane < 2 * NW)
+        lds_write16(zring + (rz & (LAP_ZL - 1)) * ZREC + lane * 16,
+                    make_uint4((uint32_t)f.z[0], (uint32_t)(f.z[0] >> 32), (uint32_t)f.z[1],
+                               (uint32_t)(f.z[1] >> 32)));
+    };
+    int32_t seen_w0 = 0, seen_wl = 0;
+    // prologue: z records ZT-2 .. ZT+ZA-1 (position 0's step-0 inputs and the
+    // z reads of steps the loader's progress does not cover), checked now
+    if (zin) {
+      for (int rz = ZT - 2; rz < ZT + ZA; ++rz) {
+        Fetch f;
+        fetch_z(rz, f);
+        if (rz < T_left && !z_ok(rz, f)) settle_z(rz, f);
+        put_z(rz, f);
+      }
+    }
+    __syncthreads();  // (matches the compute waves' prologue barrier)
+    Fetch fq[LPD];
 #pragma unroll
-        for (int i = 0; i < M; ++i) {
+    for (int j = 0; j < LPD; ++j) fetch(j, fq[j]);
+    // one step: check the fetch of step s (registers fq[j]), store it to LDS,
+    // publish, refill fq[j] with step s + LPD
+    auto lstep = [&](auto jj, int32_t s) {
+      constexpr int j = decltype(jj)::value;
+      Fetch &f = fq[j];
+      if (yin && s + YOFF < T_above && !y_ok(s, f)) settle_y(s, f);
+      const int32_t rz = s + ZT + ZA;
+      if (zin && rz < T_left && !z_ok(rz, f)) settle_z(rz, f);
+      if (lane == 0) {  // my consumers' progress, for the producing waves' back-pressure
+        bpw[0] = f.py;
+        bpw[1] = f.pz;
+      }
+      wait_word(pw, seen_w0, s - K0 + 1);                           // wave 0 is done with xr0 slot s % K0
+      wait_word(pw + 64 * (NW - 1), seen_wl, s + ZA - LAP_ZL + 1);  // the last wave with zring's old record
+      uint8_t *dst = xr0 + (s & (K0 - 1)) * SLOT + lane * REC_BYTES;
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+        lds_write16(dst + i * PAIR, make_uint4((uint32_t)f.y[2 * i], (uint32_t)(f.y[2 * i] >> 32),
+                                               (uint32_t)f.y[2 * i + 1], (uint32_t)(f.y[2 * i + 1] >> 32)));
+      put_z(rz, f);
+      lds_publish(pw + 64 * NW, s + 1, lane);  // wave 0 may run step s
+      fetch(s + LPD, f);
+    };
+    int32_t s = 0;
+#pragma unroll 1
+    for (; s + LPD <= T; s += LPD)
+      static_for<0, LPD>([&](auto jj) { LAP_INLINE(lstep(jj, s + decltype(jj)::value)); });
+    static_for<0, LPD>([&](auto jj) {
+      if (s + decltype(jj)::value < T) LAP_INLINE(lstep(jj, s + decltype(jj)::value));
+    });
+    if (lane == 0) w_stall[0] = (int32_t)stalls;
+  } else {
+    // =================== compute waves ===================
+    // a[i] of this lane at step t = sA2[t - 2w - (M lane + i) + OFF]
+    const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
+                            4u * (uint32_t)(OFF - 2 * w - M * lane - (M - 1));
+    const int32_t y0 = L * RW + 2 * w;  // rows y0 (lo) and y0 + 1 (hi), 0-based
+    const uint32_t bw = (y0 < lb ? SYM0 << (seqs[o1 + y0] & 3) : 0u) |
+                        ((y0 + 1 < lb ? SYM0 << (seqs[o1 + y0 + 1] & 3) : 0u) << 16);
+    uint32_t bv[M], c[M], SBC[M], K_[M], DMC[M];
+    uint32_t oIx[M], shIz[M], svIxy[M], svIyz[M], shIxz[2][M], svM[2][M];
+    uint32_t pIy[M], pIxy[M], pIyz[M], pBest[M];  // this wave's record of the previous step
+    {
+      uint32_t one1 = 0x00010001u, sbcv = pa.h_sbc, kdv = pa.h_kd, k0v = pa.h_k0;
+      asm volatile("" : "+v"(one1), "+v"(sbcv), "+v"(kdv), "+v"(k0v));
+      const int64_t oc = o2 + (int64_t)q * ZT;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const int k = M * lane + i;
+        c[i] = (k < zt_q ? SYM0 << (seqs[oc + k] & 3) : 0u) * 0x00010001u;
+        DMC[i] = dm_over_code(pa.dmf, c[i]);
+        bv[i] = bw;
+        const uint32_t e01 = pk_eq1(bw, c[i], one1);
+        SBC[i] = pk_mad(e01, sbcv, 0u);
+        K_[i] = pk_mad(e01, kdv, k0v);
+        oIx[i] = shIz[i] = pa.f_single;
+        shIxz[0][i] = shIxz[1][i] = svIxy[i] = svIyz[i] = pa.f_pair;
+        svM[0][i] = svM[1][i] = 0;
+        pIy[i] = pIxy[i] = pIyz[i] = pBest[i] = 0;
+      }
+    }
+    uint32_t Q = F16 ? 0x08000800u : 0x00010001u, fsv = pa.f_single, fpv = pa.f_pair;
+    uint32_t mlo = 0x0000FFFFu, mhi = 0xFFFF0000u;
+    asm volatile("" : "+v"(Q), "+v"(fsv), "+v"(fpv), "+v"(mlo), "+v"(mhi));
+    const PencilArgs pv = F16 ? pa : pin_score_consts(pa);
+    const uint32_t sel0 = lane == 0 ? 0x03020100u : 0x07060504u;  // lane 0: whole word from the face
+    __syncthreads();  // the loader's prologue z records are in LDS
+    if (zin) {  // position 0 before step 0 (tools/lap_emu.py: the same initial shifts)
+      const uint8_t *r1 = zring + ((ZT - 1) & (LAP_ZL - 1)) * ZREC + w * LAP_ZREC_WAVE;
+      const uint8_t *r2 = zring + ((ZT - 2) & (LAP_ZL - 1)) * ZREC + w * LAP_ZREC_WAVE;
+      const uint4 a0 = lds_read16(r1), a1 = lds_read16(r1 + 16);
+      const uint4 b0 = lds_read16(r2), b1 = lds_read16(r2 + 16);
+      if (lane == 0) {
+        shIz[0] = a0.x;
+        svIyz[0] = a1.x;
+        shIxz[1][0] = a0.z;
+        svM[1][0] = a1.z;
+        shIxz[0][0] = b0.z;
+        svM[0][0] = b1.z;
+      }
+    }
+    unsigned long long clk0 = 0;
+    if (trace != nullptr) {
+      stamp(1, now());
+      clk0 = __builtin_amdgcn_s_memtime();  // shader clock: the loop's cycles (slot 6)
+    }
+    // wave 0's y input: xr0 slot t % K0, or the face record (stride 0)
+    const uint8_t *const ysrc = (yin ? xr0 : yface) + lane * REC_BYTES;
+    const int32_t ystride = yin ? SLOT : 0;
+    // position 0's z input: zring slot (t + ZT) % ZL, or the face record
+    const uint8_t *const zsrc = (zin ? zring : zface) + w * LAP_ZREC_WAVE;
+    const int32_t zstride = zin ? ZREC : 0;
+    uint32_t a_nx[M];
+    load_a<M>(a_lane, a_nx);
+    // producer side: my consumers' progress (y: the lap below, via the last
+    // wave; z: the tile to the right, every wave), LDS-DMA'd by the loader
+    int32_t seen_in = 0, seen_out = 0, seen_y = 0, seen_z = 0;
+    uint32_t n_bp = 0;
+#if defined(TSA_LAP_PROF)  // shader cycles: reads + pre-cell, check, post + stores, step gap
+    uint64_t prof[4] = {0, 0, 0, 0}, prof_last = 0;
+#endif
+    constexpr int LM = M == 1 ? 0 : M == 2 ? 1 : M == 4 ? 2 : 3;  // log2 M
+    int32_t klo = -2 * w, ihi = 0;  // x = 1 position of the low half at the current step
+    uint64_t lm_hi = 0;             // the high half's lane mask (previous step's low)
+    auto prog_decode = [&](int32_t v) -> int32_t {
+      return ((uint32_t)v >> 13) == ep19 ? (int32_t)(v & 0x1FFF) : 0;
+    };
+    auto wait_consumer = [&](int64_t cons, int32_t &seen, int32_t *word, int32_t need) {
+      if (need <= seen) return;
+      seen = max(seen, prog_decode(lds_word(word)));
+      if (need <= seen) return;
+      ++n_bp;
+      for (uint32_t spin = 0;; ++spin) {
+        const int32_t v = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(prog + cons * LAP_PROG_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        seen = max(seen, prog_decode(v));
+        if (need <= seen) return;
+        if (spin >= spin_limit || timed_out || ((spin & 63) == 63 && lds_word(w_abort) != 0)) {
+          fail();
+          seen = 1 << 24;
+          return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    };
+    const int64_t cons_y = yout ? lid + GZ : -1, cons_z = zout ? lid + 1 : -1;
+
+    // ROLE: 0 = wave 0, 1 = middle waves, 2 = the last wave (NW >= 2)
+    auto step = [&](auto ph, auto role, int32_t t, auto fin_step) {
+      constexpr int PH = decltype(ph)::value;
+      constexpr int ROLE = decltype(role)::value;
+      constexpr bool FIN = decltype(fin_step)::value;
+      uint32_t a[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) a[i] = a_nx[i];
+      load_a<M>(a_lane + 4u * (uint32_t)(t + 1), a_nx);
+      // ---- input reads, issued first: the producer's progress word (unless the
+      // cached value covers step t), then its record. LDS executes a wave's DS
+      // instructions in order, so a word read that covers t proves the record
+      // read behind it current; the check waits until the pre-cell is done.
+#if defined(TSA_LAP_PROF)
+      const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+#endif
+      const int32_t need = ROLE == 0 ? t + 1 : t;
+      const int32_t *const pword = ROLE == 0 ? pw + 64 * NW : pw + 64 * (w - 1);
+      const bool waits = ROLE != 0 || yin || zin;
+      const bool poll = waits && seen_in < need;
+      int32_t fl_v = 0;
+      if (poll)
+        fl_v = *(volatile const __attribute__((address_space(3))) int32_t *)(
+            const __attribute__((address_space(3))) void *)pword;
+      asm volatile("" ::: "memory");
+      const uint8_t *src = ROLE == 0 ? ysrc + (t & (K0 - 1)) * ystride
+                                     : xr + ((w - 1) * K + ((t - 1) & (K - 1))) * SLOT + lane * REC_BYTES;
+      uint4 rv[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) rv[i] = lds_read16(src + i * PAIR);
+      // the successor's progress, read now and consulted before the record store
+      int32_t succ_v = 0;
+      if constexpr (ROLE != 2)
+        succ_v = *(volatile const __attribute__((address_space(3))) int32_t *)(
+            const __attribute__((address_space(3))) void *)(pw + 64 * (w + 1));
+      // position 0's z-1 neighbour for the next step: the z = 0 face, or the
+      // left tile's record t + ZT (checked by the loader: see ZA)
+      // (four 4-byte reads, merged into two ds_read2_b32: reading the tags too
+      // hands the compiler dead registers it reuses, forcing lgkmcnt(0) waits)
+      const uint8_t *zr = zsrc + ((t + ZT) & (LAP_ZL - 1)) * zstride;
+      auto lds32 = [](const uint8_t *p) {
+        return *(const __attribute__((address_space(3))) uint32_t *)(
+            const __attribute__((address_space(3))) void *)p;
+      };
+      const uint32_t fIz = lds32(zr), fIxz = lds32(zr + 8), fIyz = lds32(zr + 16), fM = lds32(zr + 24);
+      uint32_t inIx[M], inIz[M], inIxy[M], inIyz[M], inIxz[M], inM[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        inIx[i] = oIx[i];
+        inIz[i] = shIz[i];
+        inIxy[i] = svIxy[i];
+        inIyz[i] = svIyz[i];
+        inIxz[i] = shIxz[PH][i];
+        inM[i] = svM[PH][i];
+      }
+      // ---- x = 1: low half at position klo = t - 2w, high half one position
+      // behind (= the low half's position of the previous step); their x - 1
+      // inputs are the x = 0 face (src/PE_1cyc.v:164-178,196-218). Branch-free:
+      // SALU lane masks (zero outside the tile) and one bfi mask per register.
+      const uint64_t lm_lo = lane_bit(klo >> LM);
+      const int32_t ilo = klo & (M - 1);
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const uint64_t ml = (M == 1 || ilo == i) ? lm_lo : 0ull;
+        const uint64_t mh = (M == 1 || ihi == i) ? lm_hi : 0ull;
+        uint32_t m0, m1;
+        asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(m0) : "v"(mhi), "s"(mh));
+        asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(m1) : "v"(m0), "v"(mlo), "s"(ml));
+        inIx[i] = vbfi(m1, fsv, inIx[i]);
+        inIxy[i] = vbfi(m1, fpv, inIxy[i]);
+        inIxz[i] = vbfi(m1, fpv, inIxz[i]);
+        inM[i] = vbfi(m1, 0u, inM[i]);
+      }
+      lm_hi = lm_lo;
+      ihi = ilo;
+      ++klo;
+      // ---- the cell, up to the row above
+      LapPre<M> pre;
+      if constexpr (F16)
+        lap_pre_f16<M, SOP>(a, bv, c, SBC, K_, DMC, Q, pa, inIx, inIz, inIxy, inIyz, inIxz, inM, pre);
+      else
+        lap_pre_i16<M, SOP>(a, bv, c, Q, pv, inIx, inIz, inIxy, inIyz, inIxz, inM, pre);
+      // pin the pre-cell here: left alone the compiler sinks it below the
+      // progress check, so the record read's latency would not be covered
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+        asm volatile("" : "+v"(pre.W[i]), "+v"(pre.N1[i]), "+v"(pre.N2[i]), "+v"(pre.N3[i]),
+                     "+v"(pre.N4[i]), "+v"(pre.N5[i]), "+v"(pre.N6[i]));
+#if defined(TSA_LAP_PROF)
+      const uint64_t pt1 = __builtin_amdgcn_s_memtime();
+#endif
+      // ---- the input record is current? (slow path: poll, then read it again)
+      if (poll) {
+        seen_in = max(seen_in, (int32_t)__builtin_amdgcn_readfirstlane(fl_v));
+        if (seen_in < need) {
+          wait_word(pword, seen_in, need);
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int i = 0; i < M; ++i) rv[i] = lds_read16(src + i * PAIR);
+        }
+      }
+      // ---- the row above of both halves
+      uint32_t Ry[M], Rxy[M], Ryz[M], Rb[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        if constexpr (ROLE != 0) {  // wave w-1's high halves
+          Ry[i] = rows2(pIy[i], rv[i].x);
+          Rxy[i] = rows2(pIxy[i], rv[i].y);
+          Ryz[i] = rows2(pIyz[i], rv[i].z);
+          Rb[i] = rows2(pBest[i], rv[i].w);
+        } else {  // tagged record {Iy.hi | Ixy.hi << 16, tag, Iyz.hi | best.hi << 16, tag}
           Ry[i] = perm(pIy[i], rv[i].x, 0x05040100u);
           Rxy[i] = perm(pIxy[i], rv[i].x, 0x05040302u);
           Ryz[i] = perm(pIyz[i], rv[i].z, 0x05040100u);
           Rb[i] = perm(pBest[i], rv[i].z, 0x05040302u);
         }
-      } else {  // y = 0 face above row 1
-#pragma unroll
-        for (int i = 0; i < M; ++i) {
-          Ry[i] = rows2(pIy[i], face.x);
-          Rxy[i] = rows2(pIxy[i], face.y);
-          Ryz[i] = rows2(pIyz[i], face.z);
-          Rb[i] = rows2(pBest[i], face.w);
-        }
       }
-      settle_z(t + ZT + ZV);  // the z record all waves shift in ZV steps from now
-    } else {  // the record wave w-1 wrote SK steps ago
-      const uint8_t *src = xr + ((w - 1) * NSL + ((t + NSL - SK) & (NSL - 1))) * SLOT + lane * REC_BYTES;
+#if defined(TSA_LAP_PROF)
+      asm volatile("" :: "v"(Ry[0]));
+      const uint64_t pt2 = __builtin_amdgcn_s_memtime();
+#endif
+      uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
+#if defined(TSA_EXP_NOCELL)  // timing-only experiment: no cell arithmetic after the record
 #pragma unroll
       for (int i = 0; i < M; ++i) {
-        const uint4 rv = lds_read16(src + i * PAIR);
-        Ry[i] = rows2(pIy[i], rv.x);
-        Rxy[i] = rows2(pIxy[i], rv.y);
-        Ryz[i] = rows2(pIyz[i], rv.z);
-        Rb[i] = rows2(pBest[i], rv.w);
+        nIx[i] = pre.N1[i]; oIy[i] = Ry[i]; oIz[i] = pre.N3[i]; oIxy[i] = pre.N4[i];
+        oIyz[i] = pre.N5[i]; oIxz[i] = pre.N6[i]; oBest[i] = pre.W[i];
       }
-    }
-    uint32_t inIx[M], inIy[M], inIz[M], inIxy[M], inIyz[M], inIxz[M], inM[M];
+#else
+      if constexpr (F16) lap_post_f16<M>(pa, Ry, pre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
+      else lap_post_i16<M>(pv, Ry, pre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
+#endif
+      if constexpr (FIN) {  // the final cell (src/TriAlign_1cyc.v:141-142,342-345)
+        if (final_wg && w == (r_f >> 1)) {  // row r_f: half r_f & 1 of wave r_f / 2
 #pragma unroll
-    for (int i = 0; i < M; ++i) {
-      inIx[i] = oIx[i];
-      inIy[i] = Ry[i];
-      inIz[i] = shIz[i];
-      inIxy[i] = svIxy[i];
-      inIyz[i] = svIyz[i];
-      inIxz[i] = shIxz[PH][i];
-      inM[i] = svM[PH][i];
-    }
-    // ---- x = 1: low half at position t - 2w, high half one position behind;
-    // their x - 1 inputs are the x = 0 face (src/PE_1cyc.v:164-178,196-218)
-    const int32_t klo = __builtin_amdgcn_readfirstlane(t - WO * w);  // uniform: SGPR lane masks
-    if (klo >= 0 && klo <= ZT) {
-      const int32_t khi = klo - 1;
-      const uint64_t lm_lo = sgpr64(klo < ZT ? 1ull << (klo / M) : 0ull);
-      const uint64_t lm_hi = sgpr64(khi >= 0 ? 1ull << (khi / M) : 0ull);
-      const int32_t ilo = klo % M, ihi = (khi + M) % M;
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        if (M == 1 || i == ilo || i == ihi) {
-          uint32_t m1;
-          if constexpr (M == 1) {  // lanes klo and klo - 1 are different lanes
-            uint32_t mh;
-            asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(mh) : "v"(mhi), "s"(lm_hi));
-            asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(m1) : "v"(mh), "v"(mlo), "s"(lm_lo));
-          } else {  // M >= 2: one register gets at most one of the two halves
-            const uint64_t lm = i == ilo ? lm_lo : lm_hi;
-            const uint32_t hm = i == ilo ? mlo : mhi;
-            asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(m1) : "v"(hm), "s"(lm));
-          }
-          inIx[i] = vbfi(m1, fsv, inIx[i]);
-          inIxy[i] = vbfi(m1, fpv, inIxy[i]);
-          inIxz[i] = vbfi(m1, fpv, inIxz[i]);
-          inM[i] = vbfi(m1, 0u, inM[i]);
+          for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
         }
       }
-    }
-    uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (F16)
-      cell_messages_f16<M, SOP>(a, bv, c, SBC, K, DMC, Q, pa, inIx, inIy, inIz, inIxy, inIyz, inIxz,
-                                inM, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
-    else
-      cell_messages<M, SOP ? 1 : 0>(a, bv, c, Q, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM,
-                                    nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (FIN) {  // the final cell (src/TriAlign_1cyc.v:141-142,342-345)
-      if (final_wg && w == (r_f >> 1)) {  // row r_f: half r_f & 1 of wave r_f / 2
-#pragma unroll
-        for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
-      }
-    }
-    // ---- z staging: this wave's last position (lane 63, register M-1)
-    if (zout && lane == 63)
-      lds_write16(zst + ((t & 3) * NW + w) * 16,
-                  make_uint4(oIz[M - 1], oIxz[M - 1], Ryz[M - 1], Rb[M - 1]));
-    // ---- records: to the wave below, or (last wave) the y ring and z ring
-    if constexpr (ROLE != 2) {
-      uint8_t *dst = xr + (w * NSL + (t & (NSL - 1))) * SLOT + lane * REC_BYTES;
-#pragma unroll
-      for (int i = 0; i < M; ++i)
-        lds_write16(dst + i * PAIR, make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
-    } else {
-      if (yout) {
-        wait_consumer(cons_y, seen_y, bpw, t - YR - YOFF);
-        const uint32_t tg = lap_tag(epoch, t);
+      // ---- records: to the wave below (LDS), or (last wave) the y ring
+      if constexpr (ROLE != 2) {
+        seen_out = max(seen_out, (int32_t)__builtin_amdgcn_readfirstlane(succ_v));
+        wait_word(pw + 64 * (w + 1), seen_out, t - K + 2);  // wave w+1 read slot t % K's old record
+        uint8_t *dst = xr + (w * K + (t & (K - 1))) * SLOT + lane * REC_BYTES;
 #pragma unroll
         for (int i = 0; i < M; ++i)
-          store16_sc1(yf_mine + ((int64_t)(t & (YR - 1)) * M + i) * PAIR + lane * REC_BYTES,
-                      make_uint4(perm(oIxy[i], oIy[i], 0x07060302u), tg,
-                                 perm(oBest[i], oIyz[i], 0x07060302u), tg));
+          lds_write16(dst + i * PAIR, make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
+      } else {
+        if (yout) {
+          wait_consumer(cons_y, seen_y, bpw, t - YR - YOFF + 1);
+          const uint32_t tg = lap_tag(epoch, t);
+#pragma unroll
+          for (int i = 0; i < M; ++i)
+            store16_sc1(yf_mine + ((int64_t)(t & (YR - 1)) * M + i) * PAIR + lane * REC_BYTES,
+                        make_uint4(perm(oIxy[i], oIy[i], 0x07060302u), tg,
+                                   perm(oBest[i], oIyz[i], 0x07060302u), tg));
+        }
+        // my producers' back-pressure: the loader has checked at least
+        // t - NW + 2 steps (wave 0 ran t - NW + 1 before this wave's step t)
+        if ((yin || zin) && (t & (LAP_PUB - 1)) == 0 && lane == 0)
+          __hip_atomic_store(prog + lid * LAP_PROG_STRIDE,
+                             (int32_t)((ep19 << 13) | (uint32_t)max(t - NW + 2, 0)),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (zout && t >= SK) {  // z record of step t-SK: complete in LDS since the last barrier
-        const int32_t s = t - SK;
-        wait_consumer(cons_z, seen_z, bpw + 1, s - ZR - ZT - ZV);
-        if (lane < 2 * NW) {
-          const uint32_t tg = lap_tag(epoch, s);
-          const uint4 v = lds_read16(zst + ((s & 3) * NW + (lane >> 1)) * 16);
-          const uint4 o = (lane & 1) ? make_uint4(v.z, tg, v.w, tg) : make_uint4(v.x, tg, v.y, tg);
-          store16_sc1(zf_mine + (int64_t)(s & (ZR - 1)) * ZREC + lane * 16, o);
+      // ---- z record of this wave's last position (lane 63, register M-1)
+      if (zout) {
+        wait_consumer(cons_z, seen_z, bpw + 1, t - ZR - ZT - ZA + 1);
+        if (lane == 63) {
+          const uint32_t tg = lap_tag(epoch, t);
+          uint8_t *zdst = zf_mine + (int64_t)(t & (ZR - 1)) * ZREC + w * LAP_ZREC_WAVE;
+          store16_sc1(zdst, make_uint4(oIz[M - 1], tg, oIxz[M - 1], tg));
+          store16_sc1(zdst + 16, make_uint4(Ryz[M - 1], tg, Rb[M - 1], tg));
         }
       }
-      if ((t & 7) == 0 && lane == 0) {  // refresh the consumers' progress words
-        if (yout) dma4(prog + cons_y * LAP_PROG_STRIDE, bpw);
-        if (zout) dma4(prog + cons_z * LAP_PROG_STRIDE, bpw + 1);
+      lds_publish(pw + 64 * w, t + 1, lane);
+#if defined(TSA_LAP_PROF)
+      const uint64_t pt3 = __builtin_amdgcn_s_memtime();
+      prof[0] += pt1 - pt0;
+      prof[1] += pt2 - pt1;
+      prof[2] += pt3 - pt2;
+      prof[3] += prof_last ? pt0 - prof_last : 0;
+      prof_last = pt3;
+#endif
+      // ---- advance the systolic registers
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        oIx[i] = nIx[i];
+        svIxy[i] = Rxy[i];
+        pIy[i] = oIy[i];
+        pIxy[i] = oIxy[i];
+        pIyz[i] = oIyz[i];
+        pBest[i] = oBest[i];
+      }
+      zshift<M>(shIxz[PH], oIxz, sel0, fIxz);
+      zshift<M>(shIz, oIz, sel0, fIz);
+      zshift<M>(svIyz, Ryz, sel0, fIyz);
+      zshift<M>(svM[PH], Rb, sel0, fM);
+    };
+    auto run = [&](auto role) {  // the last step peeled off (it records the final cell)
+      int32_t t = 0;
+      const int32_t T1 = T - 1;
+      constexpr std::integral_constant<int, 0> P0{};
+      constexpr std::integral_constant<int, 1> P1{};
+      constexpr std::false_type mid{};
+      constexpr std::true_type last{};
+#pragma unroll 1
+      for (; t + 1 < T1; t += 2) {
+        LAP_INLINE(step(P0, role, t, mid));
+        LAP_INLINE(step(P1, role, t + 1, mid));
+      }
+      if (t < T1) {
+        LAP_INLINE(step(P0, role, t, mid));
+        LAP_INLINE(step(P1, role, t + 1, last));
+      } else {
+        LAP_INLINE(step(P0, role, t, last));
+      }
+    };
+    static_assert(NW >= 2, "wave 0 and the last wave are distinct roles");
+#if defined(TSA_EXP_ALLMID)  // timing-only experiment: every wave runs the middle role
+    LAP_INLINE(run(std::integral_constant<int, 1>{}));
+#else
+    if (w == 0) LAP_INLINE(run(std::integral_constant<int, 0>{}));
+    else if (w == NW - 1) LAP_INLINE(run(std::integral_constant<int, 2>{}));
+    else LAP_INLINE(run(std::integral_constant<int, 1>{}));
+#endif
+    if (trace != nullptr) {
+      const unsigned long long clk1 = __builtin_amdgcn_s_memtime();
+      stamp(2, now());
+      if (threadIdx.x == 0) {
+        trace[(int64_t)b * LAP_TRACE_SLOTS + 5] = n_wait;
+        trace[(int64_t)b * LAP_TRACE_SLOTS + 6] = clk1 - clk0;
       }
     }
-    // ---- advance the systolic registers
-#pragma unroll
-    for (int i = 0; i < M; ++i) {
-      oIx[i] = nIx[i];
-      svIxy[i] = Rxy[i];
-      pIy[i] = oIy[i];
-      pIxy[i] = oIxy[i];
-      pIyz[i] = oIyz[i];
-      pBest[i] = oBest[i];
-    }
-    // position 0's z-1 neighbour: the z = 0 face, or the left tile's record t + ZT
-    uint32_t fIz = pa.f_single, fIxz = pa.f_pair, fIyz = pa.f_pair, fM = 0u;
-    if (zin) {
-      const uint8_t *zr = zring + ((t + ZT) & (LAP_ZL - 1)) * ZREC + w * LAP_ZREC_WAVE;
-      const uint4 z0 = lds_read16(zr), z1 = lds_read16(zr + 16);
-      fIz = z0.x;
-      fIxz = z0.z;
-      fIyz = z1.x;
-      fM = z1.z;
-    }
-    zshift<M>(shIxz[PH], oIxz, sel0, fIxz);
-    zshift<M>(shIz, oIz, sel0, fIz);
-    zshift<M>(svIyz, Ryz, sel0, fIyz);
-    zshift<M>(svM[PH], Rb, sel0, fM);
-    if constexpr (ROLE == 0) {
-      fetch_y(t + LPD);
-      fetch_z(t + LPD + ZT + ZV);
-    }
-    // progress of this workgroup as a consumer: by the last barrier (t-1 is
-    // odd) wave 0 had landed and checked the y records <= (t-1) + YOFF and the z
-    // records <= (t-1) + ZT + ZV; published as t (decoded: step t-1 complete)
-    if constexpr (ROLE == 1) {
-      if (w == 1 && (t & (LAP_PUB - 1)) == 0 && lane == 0 && (yin || zin))
-        __hip_atomic_store(prog + lid * LAP_PROG_STRIDE, (int32_t)((ep19 << 13) | (uint32_t)t),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if constexpr (SK == 1 || PH == 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  };
-  auto run = [&](auto role) {  // the last step peeled off (it records the final cell)
-    int32_t t = 0;
-    const int32_t T1 = T - 1;
-    constexpr std::integral_constant<int, 0> P0{};
-    constexpr std::integral_constant<int, 1> P1{};
-    constexpr std::false_type mid{};
-    constexpr std::true_type last{};
-#pragma unroll 1
-    for (; t + 1 < T1; t += 2) {
-      LAP_INLINE(step(P0, role, t, mid));
-      LAP_INLINE(step(P1, role, t + 1, mid));
-    }
-    if (t < T1) {
-      LAP_INLINE(step(P0, role, t, mid));
-      LAP_INLINE(step(P1, role, t + 1, last));
-    } else {
-      LAP_INLINE(step(P0, role, t, last));
-    }
-  };
-  static_assert(NW >= 2, "wave 1 publishes the progress");
-  if (w == 0) LAP_INLINE(run(std::integral_constant<int, 0>{}));
-  else if (w == NW - 1) LAP_INLINE(run(std::integral_constant<int, 2>{}));
-  else LAP_INLINE(run(std::integral_constant<int, 1>{}));
-  if (trace != nullptr) {
-    stamp(2, now());
-    if (threadIdx.x == 0) {
-      trace[(int64_t)b * 8 + 4] = n_stall;
-      trace[(int64_t)b * 8 + 5] = n_bp;
-    }
-  }
-  // the z records of the last SK steps and the final cell: staged before this barrier
-  __syncthreads();
-  if (w == NW - 1 && zout && lane < 2 * NW) {
-    for (int32_t s = max(T - SK, 0); s < T; ++s) {
-      wait_consumer(cons_z, seen_z, bpw + 1, s - ZR - ZT - ZV);
-      const uint32_t tg = lap_tag(epoch, s);
-      const uint4 v = lds_read16(zst + ((s & 3) * NW + (lane >> 1)) * 16);
-      const uint4 o = (lane & 1) ? make_uint4(v.z, tg, v.w, tg) : make_uint4(v.x, tg, v.y, tg);
-      store16_sc1(zf_mine + (int64_t)(s & (ZR - 1)) * ZREC + lane * 16, o);
-    }
+    if (w == NW - 1 && lane == 0) w_bp[0] = (int32_t)n_bp;
+#if defined(TSA_LAP_PROF)
+    if (trace != nullptr && lane == 0 && w < 8)
+      for (int k = 0; k < 4; ++k) trace[(int64_t)b * LAP_TRACE_SLOTS + 8 + 4 * w + k] = prof[k];
+#endif
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // the final cell and the loader's counters are in LDS
+  if (trace != nullptr && threadIdx.x == 0) {
+    trace[(int64_t)b * LAP_TRACE_SLOTS + 4] = (unsigned long long)w_stall[0];
+    trace[(int64_t)b * LAP_TRACE_SLOTS + 7] = (unsigned long long)w_bp[0];
+  }
   if (final_wg && threadIdx.x == 0) {
     const int32_t kf = k_f, hf = r_f & 1;
     const uint32_t v = fin[(kf % M) * 64 + kf / M];
@@ -626,10 +932,10 @@ static int lap_blocks_per_cu_t(size_t lds) {
   int nb = 0;
   int dev = -1;
   if (hipGetDevice(&dev) == hipSuccess &&
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lap_kernel<M, NW, F16, SOP>, 64 * NW,
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lap_kernel<M, NW, F16, SOP>, 64 * (NW + 1),
                                                    lds) == hipSuccess)
     return nb;
-  return (int)std::min<size_t>(LDS_MAX / std::max<size_t>(lds, 1), 32 / NW);
+  return (int)std::min<size_t>(LDS_MAX / std::max<size_t>(lds, 1), 32 / (NW + 1));
 }
 #define TSA_LAP_SHAPES(FN, M_, NW_, F16_, SOP_, ...)                                          \
   ((M_) == 1 ? ((NW_) == 4 ? TSA_ARITH(FN, 1, 4, F16_, SOP_, __VA_ARGS__)                      \
@@ -640,11 +946,12 @@ static int lap_blocks_per_cu_t(size_t lds) {
                              : TSA_ARITH(FN, 4, 8, F16_, SOP_, __VA_ARGS__)))
 
 // Step time (us) along the chain, fitted to single-cube runs on MI355X
-// (scripts/gpu_lap.sh): 64^3..512^3 with one workgroup per CU
-// give 0.48-0.56 (M = 1), 0.62-0.67 (M = 2), 0.81 (M = 4); 1024^3 with 2-4
-// workgroups per CU 0.84-0.87 -- the chain steps include the hand-off stalls.
+// (scripts/gpu_lapvar.sh, tools/lap_trace.py): 64^3..512^3 at
+// M = 1 give 0.34-0.45 (NW = 4) and 0.42-0.48 (NW = 8), growing with the
+// workgroups per CU; M = 2 / 4 carry the round-1 fits scaled the same way --
+// the chain steps include the hand-off stalls.
 static double lap_step_us(int M, int NW, int64_t wg_per_cu) {
-  const double base = M == 1 ? (NW == 4 ? 0.50 : 0.52) : M == 2 ? 0.65 : 0.82;
+  const double base = M == 1 ? (NW == 4 ? 0.36 : 0.44) : M == 2 ? 0.55 : 0.72;
   return base * (1.0 + 0.22 * (double)(std::max<int64_t>(wg_per_cu, 1) - 1));
 }
 
@@ -658,7 +965,7 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   g.GZ = (max_lc + ZT - 1) / ZT;
   g.NC = n * g.GZ;             // columns: (triple, z-tile)
   g.CH = (g.NC + 7) / 8;       // columns per XCD
-  const int YOFF = (LAP_SK + 1) * (NW - 1) + 1;  // lap lag of a record (kernel: YOFF)
+  const int YOFF = 2 * (NW - 1) + 1;  // lap lag of a record (kernel: YOFF)
   const int32_t T = max_la + YOFF + ZT;  // >= every workgroup's step count
   auto pow2 = [](int64_t v) { int64_t p = 1; while (p < v) p <<= 1; return (int32_t)p; };
   g.YR = full_rings ? pow2(T) : pow2(YOFF + LPD + 48);
@@ -680,7 +987,10 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   g.waves = per_cu > 0 ? std::max<int64_t>((wg_per_xcd + slots_xcd - 1) / slots_xcd,
                                            (wgs + (int64_t)cus * per_cu - 1) / ((int64_t)cus * per_cu))
                        : 0;
-  g.ok = per_cu > 0 && (g.G >= 2 || g.GZ >= 2);
+  // one workgroup is the helix's job; TSA_LAP_SINGLE=1 allows it (diagnostics:
+  // the step time with no hand-off)
+  const bool single = getenv("TSA_LAP_SINGLE") && atoi(getenv("TSA_LAP_SINGLE")) != 0;
+  g.ok = per_cu > 0 && (g.G >= 2 || g.GZ >= 2 || single);
   // estimated latency (us): the chain to the final workgroup -- each lap adds
   // YOFF + LPD + ~3 steps, each tile ZT + LPD + ~2 -- plus its own steps;
   // several workgroups on one CU share its SIMDs. A grid beyond the resident
@@ -723,28 +1033,35 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
   uint8_t *zf = yf + g.yf_bytes;
   unsigned long long *trace = nullptr;
   const char *tpath = getenv("TSA_LAP_TRACE");  // diagnostic: per-WG timestamps to a CSV file
-  if (tpath && hipMalloc(&trace, (size_t)g.blocks * 8 * 8) != hipSuccess) return TSA_ENOMEM;
-  if (trace && hipMemsetAsync(trace, 0, (size_t)g.blocks * 8 * 8, stream) != hipSuccess)
+  const size_t tbytes = (size_t)g.blocks * LAP_TRACE_SLOTS * 8;
+  if (tpath && hipMalloc(&trace, tbytes) != hipSuccess) return TSA_ENOMEM;
+  if (trace && hipMemsetAsync(trace, 0, tbytes, stream) != hipSuccess)
     return TSA_EDEVICE;
   const uint32_t epoch = lap_next_epoch();
-  hipLaunchKernelGGL(kfn, dim3((uint32_t)g.blocks), dim3(64 * NW), g.lds, stream, d_seqs,
+  hipLaunchKernelGGL(kfn, dim3((uint32_t)g.blocks), dim3(64 * (NW + 1)), g.lds, stream, d_seqs,
                      d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, prog, err, d_scores, pa, epoch,
                      lap_spin_limit(), trace);
   if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
   if (trace) {
-    std::vector<unsigned long long> h((size_t)g.blocks * 8);
+    std::vector<unsigned long long> h((size_t)g.blocks * LAP_TRACE_SLOTS);
     if (hipMemcpyAsync(h.data(), trace, h.size() * 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
         hipStreamSynchronize(stream) != hipSuccess)
       return TSA_EDEVICE;
     (void)hipFree(trace);
     if (FILE *fp = fopen(tpath, "w")) {
-      fprintf(fp, "block,tri,lap,tile,start,loop_begin,loop_end,xcc,stalls,bp_waits\n");
+      fprintf(fp, "block,tri,lap,tile,start,loop_begin,loop_end,xcc,stalls,w0_waits,loop_clk,bp_waits");
+      for (int k = 8; k < LAP_TRACE_SLOTS; ++k)  // TSA_LAP_PROF: wave (k-8)/4, phase (k-8)%4
+        fprintf(fp, ",prof%d_%d", (k - 8) / 4, (k - 8) % 4);
+      fprintf(fp, "\n");
       for (int64_t b = 0; b < g.blocks; ++b) {
-        if (h[b * 8] == 0) continue;  // padding block
+        const unsigned long long *hb = h.data() + b * LAP_TRACE_SLOTS;
+        if (hb[0] == 0) continue;  // padding block
         const int64_t slot = b >> 3, col = (slot % g.CH) * 8 + (b & 7);
-        fprintf(fp, "%lld,%lld,%lld,%lld,%llu,%llu,%llu,%llu,%llu,%llu\n", (long long)b,
-                (long long)(col / g.GZ), (long long)(slot / g.CH), (long long)(col % g.GZ), h[b * 8],
-                h[b * 8 + 1], h[b * 8 + 2], h[b * 8 + 3], h[b * 8 + 4], h[b * 8 + 5]);
+        fprintf(fp, "%lld,%lld,%lld,%lld,%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu", (long long)b,
+                (long long)(col / g.GZ), (long long)(slot / g.CH), (long long)(col % g.GZ), hb[0],
+                hb[1], hb[2], hb[3], hb[4], hb[5], hb[6], hb[7]);
+        for (int k = 8; k < LAP_TRACE_SLOTS; ++k) fprintf(fp, ",%llu", hb[k]);
+        fprintf(fp, "\n");
       }
       fclose(fp);
     }

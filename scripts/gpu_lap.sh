@@ -24,5 +24,4 @@ for n in 4 16 32; do
     > gpurun_out/lapn_$n.json 2> gpurun_out/lapn_$n.err || { tail -5 gpurun_out/lapn_$n.err; exit 1; }
   echo "n=$n"; cat gpurun_out/lapn_$n.json
 done
-TSA_LAP_TRACE=gpurun_out/lap_trace_256.csv timeout -k 10 120 python tools/bench_variants.py --n 1 --L 256 --rounds 1 \
-  --variants TSA_PENCIL_MODE=lap > /dev/null 2>&1; echo "trace rc=$?"
+timeout -k 10 120 python tools/lap_trace.py 64 128 256 > gpurun_out/lap_trace.jsonl; echo "trace rc=$?"

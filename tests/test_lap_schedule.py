@@ -34,3 +34,33 @@ def test_lap_schedule_vs_oracle(orc, shape, nw, m, kind, sk):
     sop = bool(rng.integers(0, 2))
     op = orc.default_params(score_bits=16, s3_mode=int(sop))
     assert emulate(a, b, c, sop=sop, NW=nw, M=m, SK=sk) == orc.score(a, b, c, op)
+
+
+def test_lap_split_cell_algebra():
+    """csrc/lap_kernel.hip:lap_pre_*/lap_post_* fold every message to
+    max(Y - c, N) with the N's independent of the row above (Y = Iy's input);
+    with GO >= GE that equals the grouped message form of cell_messages_f16
+    (pencil_common.h) for any inputs -- checked exhaustively over a random
+    sample of integer inputs, penalties and folded mismatch."""
+    rng = np.random.default_rng(7)
+    for _ in range(20000):
+        ge = int(rng.integers(0, 7))
+        go = int(rng.integers(ge, 10))
+        mm = int(rng.integers(-3, 2))
+        E, O, E2, OE, O2 = ge - mm, go - mm, 2 * ge, go + ge, 2 * go
+        X, Y, Z, XY, XZ, YZ, Mv = (int(v) for v in rng.integers(-40, 40, 7))
+        S3 = max(X, Y, Z)
+        A1, A2, A3 = max(S3, XY, XZ), max(S3, YZ, XY), max(YZ, XZ, S3)
+        C1, C2, C3 = max(X, XY, Y), max(Y, YZ, Z), max(Z, XZ, X)
+        best = max(A1, YZ, Mv)
+        ref = (best, max(X - E2, A1 - OE, best - O2), max(Y - E2, A2 - OE, best - O2),
+               max(Z - E2, A3 - OE, best - O2), max(C1 - E, best - O), max(C2 - E, best - O),
+               max(C3 - E, best - O))
+        pXZ = max(X, Z)
+        U1, U2, U3 = max(pXZ, XY, XZ), max(pXZ, XY, YZ), max(pXZ, YZ, XZ)
+        W = max(U1, YZ, Mv)
+        N = (max(X - E2, U1 - OE, W - O2), max(U2 - OE, W - O2), max(Z - E2, U3 - OE, W - O2),
+             max(max(X, XY) - E, W - O), max(max(YZ, Z) - E, W - O), max(max(pXZ, XZ) - E, W - O))
+        got = (max(Y, W), max(Y - OE, N[0]), max(Y - E2, N[1]), max(Y - OE, N[2]),
+               max(Y - E, N[3]), max(Y - E, N[4]), max(Y - O, N[5]))
+        assert got == ref

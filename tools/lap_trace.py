@@ -1,50 +1,144 @@
 #!/usr/bin/env python3
-"""Single-cube lap-kernel timeline (TSA_LAP_TRACE): per (lap, tile) workgroup
-start / loop-begin / loop-end in microseconds from the first workgroup start,
-and the per-lap hand-off delay (loop begin of lap L+1 minus lap L). Run on the
-GPU box: python tools/lap_trace.py [L] [score_bits]."""
+"""Single-cube lap-kernel diagnostics on the GPU box (TSA_LAP_TRACE).
+
+    python tools/lap_trace.py [--bits 12] [--reps 5] SPEC [SPEC ...]
+
+SPEC = LA[xLBxLC][:KEY=VAL,KEY=VAL...], e.g. 64, 256, 64x16x64:TSA_LAP_NW=8.
+Knobs are libtrialign environment knobs (TSA_PENCIL_MODE=lap is always set).
+Per spec one JSON line: the median event-timed latency of `reps` calls, then
+from one traced call the per-lap loop-begin lag (hand-off chain), each
+workgroup's loop time per step (us and shader-clock cycles; the clock in MHz),
+loader stalls (tag re-fetches), wave 0's missed progress polls and
+the producers' back-pressure waits. Traces land in
+gpurun_out/lap_trace_<spec>.csv."""
+import argparse
 import csv
 import json
 import os
+import re
+import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def parse_spec(spec):
+    shape, _, knobs = spec.partition(":")
+    dims = [int(v) for v in shape.split("x")]
+    la, lb, lc = (dims * 3)[:3] if len(dims) == 1 else dims
+    env = dict(kv.split("=", 1) for kv in knobs.split(",") if kv)
+    return la, lb, lc, env
+
+
+def lap_steps(la, lb, lc, lap, tile, M, NW, SK=1):
+    """Steps of workgroup (lap, tile): lap_kernel.hip's T."""
+    RW, ZT, WO = 2 * NW, 64 * M, SK + 1
+    tau = lambda r: WO * (r >> 1) + (r & 1)
+    rows = min(RW, lb - lap * RW)
+    zt = min(ZT, lc - tile * ZT)
+    return la + tau(rows - 1) + zt - 1
+
+
 def main():
-    L = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-    bits = int(sys.argv[2]) if len(sys.argv) > 2 else 12
-    import torch  # noqa: F401
+    ap = argparse.ArgumentParser()
+    ap.add_argument("specs", nargs="+")
+    ap.add_argument("--bits", type=int, default=12)
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    import torch
     import bench
     tsa = bench.load_pkg()
     import tsa_amd.synth as synth
-    path = os.path.join(ROOT, "gpurun_out", f"lap_trace_{L}.csv")
-    os.makedirs(os.path.dirname(path), exist_ok=True)
-    a, b, c = synth.triple(0, L)
-    p = tsa.TsaParams.default(score_bits=bits)
-    tsa.score(a, b, c, p, kernel="pencil")  # warm-up
-    os.environ["TSA_LAP_TRACE"] = path
-    s = tsa.score(a, b, c, p, kernel="pencil")
-    del os.environ["TSA_LAP_TRACE"]
-    rows = list(csv.DictReader(open(path)))
-    t0 = min(int(r["start"]) for r in rows)
-    us = lambda v: (int(v) - t0) / 100.0  # s_memrealtime: 100 MHz
-    laps = {}
-    for r in rows:
-        laps.setdefault(int(r["lap"]), []).append(r)
-    out = []
-    for lp in sorted(laps):
-        rs = laps[lp]
-        out.append({"lap": lp, "start": round(min(us(r["start"]) for r in rs), 2),
-                    "loop_begin": round(min(us(r["loop_begin"]) for r in rs), 2),
-                    "loop_end": round(max(us(r["loop_end"]) for r in rs), 2),
-                    "polls": sum(int(r["polls"]) for r in rs), "spins": sum(int(r["spins"]) for r in rs)})
-    ends = [o["loop_end"] for o in out]
-    print(json.dumps({"L": L, "score": s, "wgs": len(rows), "total_us": max(ends),
-                      "plan": tsa.describe_plan(1, L, L, L, p)}))
-    for o in out:
-        print(json.dumps(o))
+    out_dir = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out_dir, exist_ok=True)
+    p = tsa.TsaParams.default(score_bits=args.bits)
+    for spec in args.specs:
+        la, lb, lc, env = parse_spec(spec)
+        env.setdefault("TSA_PENCIL_MODE", "lap")
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            a, b, c = synth.triple(0, la, lb, lc)
+            seqs, offs = tsa.pack_batch([(a, b, c)])
+            d_seqs, d_offs = torch.from_numpy(seqs).cuda(), torch.from_numpy(offs).cuda()
+            d_sc = torch.zeros(1, dtype=torch.int32, device="cuda")
+            ws = tsa.workspace_size(1, la, lb, lc, p, "pencil")
+            d_ws = torch.empty(max(ws, 16), dtype=torch.uint8, device="cuda")
+            st = torch.cuda.current_stream()
+
+            def call():
+                tsa.score_batch_async(d_seqs.data_ptr(), d_offs.data_ptr(), 1, la, lb, lc,
+                                      d_sc.data_ptr(), d_ws.data_ptr(), ws, st.cuda_stream, p, "pencil")
+            call()
+            torch.cuda.synchronize()
+            times = []
+            for _ in range(args.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                call()
+                e1.record(st)
+                torch.cuda.synchronize()
+                times.append(e0.elapsed_time(e1) * 1e3)
+            score = int(d_sc.item())
+            plan = tsa.describe_plan(1, la, lb, lc, p, kernel="pencil", sync=False)
+            path = os.path.join(out_dir, "lap_trace_" + re.sub(r"[^0-9A-Za-z_=.-]", "_", spec) + ".csv")
+            os.environ["TSA_LAP_TRACE"] = path
+            call()
+            torch.cuda.synchronize()
+            del os.environ["TSA_LAP_TRACE"]
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        rec = {"spec": spec, "plan": plan, "score": score, "us_median": round(statistics.median(times), 2),
+               "us_min": round(min(times), 2)}
+        m = re.search(r"M=(\d+) NW=(\d+)", plan)
+        if m and os.path.exists(path):
+            M, NW = int(m.group(1)), int(m.group(2))
+            rows = list(csv.DictReader(open(path)))
+            t0 = min(int(r["start"]) for r in rows)
+            us = lambda v: (int(v) - t0) / 100.0  # s_memrealtime: 100 MHz
+            laps = {}
+            per_step_us, per_step_clk, mhz = [], [], []
+            for r in rows:
+                lp, tl = int(r["lap"]), int(r["tile"])
+                laps.setdefault(lp, []).append(us(r["loop_begin"]))
+                T = lap_steps(la, lb, lc, lp, tl, M, NW)
+                dt = us(r["loop_end"]) - us(r["loop_begin"])
+                clk = int(r.get("loop_clk") or 0)
+                per_step_us.append(dt / T)
+                if clk and dt > 0:
+                    per_step_clk.append(clk / T)
+                    mhz.append(clk / dt)
+            begins = [min(laps[k]) for k in sorted(laps)]
+            lags = [round(b1 - b0, 2) for b0, b1 in zip(begins, begins[1:])]
+            rec.update({
+                "wgs": len(rows), "trace_total_us": round(max(us(r["loop_end"]) for r in rows), 2),
+                "lap_lag_us": {"median": round(statistics.median(lags), 2) if lags else None,
+                               "max": max(lags) if lags else None, "first": lags[:4]},
+                "step_us": {"median": round(statistics.median(per_step_us), 4),
+                            "max": round(max(per_step_us), 4)},
+                "step_clk": round(statistics.median(per_step_clk), 1) if per_step_clk else None,
+                "clock_mhz": round(statistics.median(mhz)) if mhz else None,
+                "stalls": sum(int(r["stalls"]) for r in rows),
+                "w0_waits": sum(int(r.get("w0_waits") or 0) for r in rows),
+                "bp_waits": sum(int(r["bp_waits"]) for r in rows),
+            })
+            prof_cols = [k for k in rows[0] if k.startswith("prof")]
+            if prof_cols:  # TSA_LAP_PROF build: per-wave cycles per step (medians over workgroups)
+                prof = {}
+                for wv in range(NW):
+                    parts = []
+                    for ph in range(4):
+                        vals = [int(r[f"prof{wv}_{ph}"]) / lap_steps(la, lb, lc, int(r["lap"]), int(r["tile"]), M, NW)
+                                for r in rows]
+                        parts.append(round(statistics.median(vals), 1))
+                    prof[f"w{wv}"] = parts
+                rec["prof_clk_per_step"] = {"phases": "reads+pre, check, post+stores, gap", **prof}
+        print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
