@@ -376,18 +376,19 @@ def time_singles(args, tsa, synth, hot, dev, L, params):
     import torch
     stream = hot.stream
 
-    def one(Ls, prm, reps):
+    def one(Ls, prm, reps, kernel=None):
+        kernel = kernel or args.kernel
         sa = synth.batch(0, 1, Ls)
         s_seqs = torch.from_numpy(sa[0]).to(dev)
         s_offs = torch.from_numpy(sa[1]).to(dev)
         s_score = torch.zeros(1, dtype=torch.int32, device=dev)
-        s_ws = tsa.workspace_size(1, Ls, Ls, Ls, prm, args.kernel)
+        s_ws = tsa.workspace_size(1, Ls, Ls, Ls, prm, kernel)
         s_wsb = torch.empty(max(s_ws, 16), dtype=torch.uint8, device=dev)
 
         def sstep():
             tsa.score_batch_async(s_seqs.data_ptr(), s_offs.data_ptr(), 1, Ls, Ls, Ls,
                                   s_score.data_ptr(), s_wsb.data_ptr(), s_ws, stream.cuda_stream,
-                                  prm, args.kernel)
+                                  prm, kernel)
         sstep()
         torch.cuda.synchronize()
         times = []
@@ -401,7 +402,7 @@ def time_singles(args, tsa, synth, hot, dev, L, params):
         sms = float(np.median(times))
         r = {"ms": round(sms, 4), "gcups": round(Ls ** 3 / (sms * 1e-3) / 1e9, 3),
              "score": int(s_score.item()), "score_bits": prm.score_bits,
-             "plan": tsa.describe_plan(1, Ls, Ls, Ls, prm, kernel=args.kernel, sync=False)}
+             "plan": tsa.describe_plan(1, Ls, Ls, Ls, prm, kernel=kernel, sync=False)}
         if Ls in ASIC_MS and prm.score_bits == 12:
             r["asic_ms"] = ASIC_MS[Ls]
             r["vs_asic"] = round(ASIC_MS[Ls] / sms, 3)
@@ -416,6 +417,11 @@ def time_singles(args, tsa, synth, hot, dev, L, params):
             out["paper N=512: 512^3"] = one(512, params, 5)
             out["configs[3]: 1024^3 (16-bit words)"] = one(
                 1024, tsa.TsaParams.default(score_bits=16), 5)
+            # the RTL's own 12-bit words at 1024^3: the checked lap kernel
+            # (the score is exact, or TSA_SCORE_UNCERTIFIED and rescored by PLANE)
+            r = one(1024, params, 5, kernel="checked")
+            r["certified"] = r["score"] != tsa.SCORE_UNCERTIFIED
+            out["configs[3]: 1024^3 (12-bit RTL words, checked)"] = r
     except Exception as e:  # noqa: BLE001
         log("single-cube measurement failed:", e)
     return out

@@ -50,7 +50,9 @@ S3_SOP = 1
 KERNEL_AUTO = 0
 KERNEL_PLANE = 1
 KERNEL_PENCIL = 2
-KERNELS = {"auto": KERNEL_AUTO, "plane": KERNEL_PLANE, "pencil": KERNEL_PENCIL}
+KERNEL_CHECKED = 3
+KERNELS = {"auto": KERNEL_AUTO, "plane": KERNEL_PLANE, "pencil": KERNEL_PENCIL,
+           "checked": KERNEL_CHECKED}
 
 # testbench symbol encoding, src/TriAlign_tb.sv:42-46
 SYMBOLS = {"A": 0, "T": 1, "C": 2, "G": 3, "N": 4}
@@ -60,11 +62,13 @@ EXPORTS = (
     "tsa_default_params", "tsa_validate", "tsa_score_gpu", "tsa_score_gpu_ex",
     "tsa_score_batch", "tsa_batch_workspace_size", "tsa_score_batch_async",
     "tsa_device_count", "tsa_strerror", "tsa_version", "tsa_describe_plan", "tsa_align_gpu",
-    "tsa_fallback_count",
+    "tsa_fallback_count", "tsa_check_fallback_count",
 )
 
 # Score of a triple the device could not score (include/trialign.h).
 SCORE_INVALID = -(2 ** 31)
+# Score of a triple the checked kernel could not certify (rescore with PLANE).
+SCORE_UNCERTIFIED = -(2 ** 31) + 1
 
 # Alignment columns (tsa_align_gpu): the state of each column and which of
 # (A, B, C) it consumes -- the predecessor offsets of src/PE_1cyc.v:164-218.
@@ -134,6 +138,8 @@ def _load_lib() -> ctypes.CDLL:
                                   pp, i32p, u8p, ctypes.c_int32, i32p, i32p, ctypes.c_int32]
     lib.tsa_fallback_count.argtypes = []
     lib.tsa_fallback_count.restype = ctypes.c_int64
+    lib.tsa_check_fallback_count.argtypes = []
+    lib.tsa_check_fallback_count.restype = ctypes.c_int64
     lib.tsa_device_count.argtypes = []
     lib.tsa_strerror.argtypes = [ctypes.c_int]
     lib.tsa_strerror.restype = ctypes.c_char_p
@@ -166,6 +172,12 @@ def fallback_count() -> int:
     """Lap hand-offs that timed out on the synchronous paths so far (each was
     rescored by the helix kernel); 0 in a healthy run."""
     return int(_lib.tsa_fallback_count())
+
+
+def check_fallback_count() -> int:
+    """Triples the checked kernel could not certify on the synchronous paths
+    so far (each was rescored by the literal PLANE kernel)."""
+    return int(_lib.tsa_check_fallback_count())
 
 
 def _as_u8(seq) -> np.ndarray:

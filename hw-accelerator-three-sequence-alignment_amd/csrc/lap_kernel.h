@@ -33,8 +33,11 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
 size_t lap_workspace_bytes(const LapGeom &g);
 // Launch it. d_err (synchronous callers): the error word, cleared before the
 // launch, nonzero after it when a hand-off timed out.
+// chk (int16 form only): the checked kernel, then a certification pass that
+// turns the score of every triple outside *chk into TSA_SCORE_UNCERTIFIED.
 int lap_launch(const LapGeom &g, bool f16, bool sop, const uint8_t *d_seqs,
                const int64_t *d_offsets, int32_t n, int32_t *d_scores, void *d_ws,
-               const PencilArgs &pa, hipStream_t stream, int32_t **d_err);
+               const PencilArgs &pa, hipStream_t stream, int32_t **d_err,
+               const CheckLimits *chk = nullptr);
 
 }  // namespace tsa

@@ -310,14 +310,20 @@ __device__ __forceinline__ void static_for(F &&f) {
     [[clang::always_inline]] call; \
   } while (0)
 
-template <int M, int NW, bool F16, bool SOP>
+// CHK (int16 form only): the checked kernel -- every real cell's best is
+// folded into a per-lane max / min; each wave's extremes go to mon[tri]
+// (max) and mon[n + tri] (min) by atomics, and lap_certify() decides whether
+// any candidate of the literal RTL recurrence could have wrapped.
+template <int M, int NW, bool F16, bool SOP, bool CHK>
 __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel(
     const uint8_t *__restrict__ seqs, const int64_t *__restrict__ offs, int32_t G, int32_t GZ,
     int32_t NC, int32_t CH, int32_t YR, int32_t ZR, uint8_t *__restrict__ yf_base,
     uint8_t *__restrict__ zf_base, int32_t *__restrict__ prog, uint32_t *__restrict__ err,
-    int32_t *__restrict__ scores, PencilArgs pa, uint32_t epoch, uint32_t spin_limit,
+    int32_t *__restrict__ scores, int32_t *__restrict__ mon, PencilArgs pa, uint32_t epoch,
+    uint32_t spin_limit,
     unsigned long long *__restrict__ trace) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  static_assert(!(CHK && F16), "the checked kernel runs the int16 form");
   constexpr int RW = 2 * NW, ZT = 64 * M, LPD = lap_pd(M), K = lap_k(M), K0 = lap_k0(M);
   constexpr int PAIR = 64 * REC_BYTES, SLOT = M * PAIR;
   // wave w's rows sit at step offsets 2w (low half) and 2w + 1 (high); lap L+1
@@ -425,6 +431,10 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
     ((uint4 *)zface)[threadIdx.x] = (threadIdx.x & 1) ? make_uint4(pa.f_pair, 0u, 0u, 0u)
                                                       : make_uint4(pa.f_single, 0u, pa.f_pair, 0u);
   pw[threadIdx.x] = 0;  // blockDim = 64 (NW + 1): one word per thread
+  // the wave-to-wave rings: step 0 reads slot K-1 before any write (its cells
+  // are not real, but the checked kernel's monitor must not see stale LDS)
+  for (int j = threadIdx.x; j < (NW - 1) * K * SLOT / 16; j += 64 * (NW + 1))
+    ((uint4 *)xr)[j] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
 
   if (w == NW) {
@@ -500,11 +510,16 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
         __builtin_amdgcn_s_sleep(1);
       }
     };
+    // records beyond the producer's last step are never checked; they only
+    // feed cells past the cube, stored as zeros (the checked kernel's monitor
+    // sees those cells too, and must not see stale ring contents)
     auto put_z = [&](int32_t rz, const Fetch &f) {
+      const bool real = rz < T_left;
       if (lane < 2 * NW)
         lds_write16(zring + (rz & (LAP_ZL - 1)) * ZREC + lane * 16,
-                    make_uint4((uint32_t)f.z[0], (uint32_t)(f.z[0] >> 32), (uint32_t)f.z[1],
-                               (uint32_t)(f.z[1] >> 32)));
+                    real ? make_uint4((uint32_t)f.z[0], (uint32_t)(f.z[0] >> 32), (uint32_t)f.z[1],
+                                      (uint32_t)(f.z[1] >> 32))
+                         : make_uint4(0u, 0u, 0u, 0u));
     };
     int32_t seen_w0 = 0, seen_wl = 0;
     // prologue: z records ZT-2 .. ZT+ZA-1 (position 0's step-0 inputs and the
@@ -536,10 +551,13 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       wait_word(pw, seen_w0, s - K0 + 1);                           // wave 0 is done with xr0 slot s % K0
       wait_word(pw + 64 * (NW - 1), seen_wl, s + ZA - LAP_ZL + 1);  // the last wave with zring's old record
       uint8_t *dst = xr0 + (s & (K0 - 1)) * SLOT + lane * REC_BYTES;
+      const bool yreal = s + YOFF < T_above;
 #pragma unroll
       for (int i = 0; i < M; ++i)
-        lds_write16(dst + i * PAIR, make_uint4((uint32_t)f.y[2 * i], (uint32_t)(f.y[2 * i] >> 32),
-                                               (uint32_t)f.y[2 * i + 1], (uint32_t)(f.y[2 * i + 1] >> 32)));
+        lds_write16(dst + i * PAIR,
+                    yreal ? make_uint4((uint32_t)f.y[2 * i], (uint32_t)(f.y[2 * i] >> 32),
+                                       (uint32_t)f.y[2 * i + 1], (uint32_t)(f.y[2 * i + 1] >> 32))
+                          : make_uint4(0u, 0u, 0u, 0u));
       put_z(rz, f);
       lds_publish(pw + 64 * NW, s + 1, lane);  // wave 0 may run step s
       fetch(s + LPD, f);
@@ -581,6 +599,15 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
         svM[0][i] = svM[1][i] = 0;
         pIy[i] = pIxy[i] = pIyz[i] = pBest[i] = 0;
       }
+    }
+    // CHK: halves of real cells (row y < lb, position z < LC of the tile); the
+    // rest is masked to 0, a value the monitor's range contains anyway (faces)
+    uint32_t vmask[M], vmax[M], vmin[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const uint32_t rowm = (y0 < lb ? 0x0000FFFFu : 0u) | (y0 + 1 < lb ? 0xFFFF0000u : 0u);
+      vmask[i] = M * lane + i < zt_q ? rowm : 0u;
+      vmax[i] = vmin[i] = 0u;
     }
     uint32_t Q = F16 ? 0x08000800u : 0x00010001u, fsv = pa.f_single, fpv = pa.f_pair;
     uint32_t mlo = 0x0000FFFFu, mhi = 0xFFFF0000u;
@@ -780,6 +807,16 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       if constexpr (F16) lap_post_f16<M>(pa, Ry, pre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
       else lap_post_i16<M>(pv, Ry, pre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
 #endif
+      if constexpr (CHK) {
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          const uint32_t v = oBest[i] & vmask[i];
+          vmax[i] = pk_max(vmax[i], v);
+          vmin[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(
+                                                     __builtin_bit_cast(s16x2, vmin[i]),
+                                                     __builtin_bit_cast(s16x2, v)));
+        }
+      }
       if constexpr (FIN) {  // the final cell (src/TriAlign_1cyc.v:141-142,342-345)
         if (final_wg && w == (r_f >> 1)) {  // row r_f: half r_f & 1 of wave r_f / 2
 #pragma unroll
@@ -881,6 +918,26 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       }
     }
     if (w == NW - 1 && lane == 0) w_bp[0] = (int32_t)n_bp;
+    if constexpr (CHK) {  // the wave's extremes -> the triple's monitor words
+      int32_t mx = 0, mn = 0;
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const int32_t lo0 = (int16_t)(vmax[i] & 0xFFFF), hi0 = (int16_t)(vmax[i] >> 16);
+        const int32_t lo1 = (int16_t)(vmin[i] & 0xFFFF), hi1 = (int16_t)(vmin[i] >> 16);
+        mx = max(mx, max(lo0, hi0));
+        mn = min(mn, min(lo1, hi1));
+      }
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        mx = max(mx, __shfl_xor(mx, d));
+        mn = min(mn, __shfl_xor(mn, d));
+      }
+      if (lane == 0) {
+        const int32_t ntri = NC / GZ;
+        atomicMax(mon + tri, mx);
+        atomicMin(mon + ntri + tri, mn);
+      }
+    }
 #if defined(TSA_LAP_PROF)
     if (trace != nullptr && lane == 0 && w < 8)
       for (int k = 0; k < 4; ++k) trace[(int64_t)b * LAP_TRACE_SLOTS + 8 + 4 * w + k] = prof[k];
@@ -901,6 +958,17 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
     const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
     scores[tri] = bad ? TSA_SCORE_INVALID
                       : F16 ? (int32_t)(float)__builtin_bit_cast(_Float16, hb) : (int32_t)(int16_t)hb;
+  }
+}
+
+// Certification of the checked kernel's triples (one thread each): a score
+// stands when every best it saw lies in [best_min, best_max].
+__global__ __launch_bounds__(256) void lap_certify(const int32_t *__restrict__ mon, int32_t n,
+                                                   CheckLimits lim, int32_t *__restrict__ scores) {
+  const int32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  if (mon[i] > lim.best_max || mon[n + i] < lim.best_min) {
+    if (scores[i] != TSA_SCORE_INVALID) scores[i] = TSA_SCORE_UNCERTIFIED;
   }
 }
 
@@ -932,7 +1000,7 @@ static int lap_blocks_per_cu_t(size_t lds) {
   int nb = 0;
   int dev = -1;
   if (hipGetDevice(&dev) == hipSuccess &&
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lap_kernel<M, NW, F16, SOP>, 64 * (NW + 1),
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lap_kernel<M, NW, F16, SOP, false>, 64 * (NW + 1),
                                                    lds) == hipSuccess)
     return nb;
   return (int)std::min<size_t>(LDS_MAX / std::max<size_t>(lds, 1), 32 / (NW + 1));
@@ -974,7 +1042,9 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   if (const char *e = getenv("TSA_LAP_LDS_EXTRA")) g.lds += (size_t)atoi(e);  // diagnostic knob
   const int64_t wgs = (int64_t)n * g.G * g.GZ;
   g.blocks = (int64_t)g.G * g.CH * 8;
-  g.prog_bytes = (((size_t)wgs * LAP_PROG_STRIDE + 64) * sizeof(int32_t) + 255) & ~(size_t)255;
+  // progress words, the error word (+63 spare), the checked kernel's monitor (2 n)
+  g.prog_bytes = (((size_t)wgs * LAP_PROG_STRIDE + 64 + 2 * (size_t)n) * sizeof(int32_t) + 255) &
+                 ~(size_t)255;
   g.yf_bytes = (size_t)wgs * g.YR * M * 1024;
   g.zf_bytes = (size_t)wgs * g.ZR * NW * LAP_ZREC_WAVE;
   if (g.lds > LDS_MAX || g.blocks > 0x7FFFFFFF) return g;
@@ -1020,8 +1090,9 @@ static uint32_t lap_next_epoch() {
 template <int M, int NW, bool F16, bool SOP>
 static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                       const LapGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
-                      hipStream_t stream) {
-  auto kfn = lap_kernel<M, NW, F16, SOP>;
+                      hipStream_t stream, const CheckLimits *chk) {
+  if (chk && F16) return TSA_EINVAL;
+  auto kfn = chk ? lap_kernel<M, NW, F16, SOP, !F16> : lap_kernel<M, NW, F16, SOP, false>;
   if (g.lds > LDS_MAX) return TSA_EINVAL;
   if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)g.lds) != hipSuccess)
@@ -1029,6 +1100,10 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
   int32_t *prog = (int32_t *)d_ws;
   const int64_t wgs = (int64_t)n * g.G * g.GZ;
   uint32_t *err = (uint32_t *)(prog + wgs * LAP_PROG_STRIDE);
+  int32_t *mon = prog + wgs * LAP_PROG_STRIDE + 64;  // [max(best)] n, [min(best)] n
+  if (chk && (hipMemsetAsync(mon, 0x80, (size_t)n * 4, stream) != hipSuccess ||
+              hipMemsetAsync(mon + n, 0x7F, (size_t)n * 4, stream) != hipSuccess))
+    return TSA_EDEVICE;
   uint8_t *yf = (uint8_t *)d_ws + g.prog_bytes;
   uint8_t *zf = yf + g.yf_bytes;
   unsigned long long *trace = nullptr;
@@ -1039,8 +1114,13 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
     return TSA_EDEVICE;
   const uint32_t epoch = lap_next_epoch();
   hipLaunchKernelGGL(kfn, dim3((uint32_t)g.blocks), dim3(64 * (NW + 1)), g.lds, stream, d_seqs,
-                     d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, prog, err, d_scores, pa, epoch,
-                     lap_spin_limit(), trace);
+                     d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, prog, err, d_scores, mon, pa,
+                     epoch, lap_spin_limit(), trace);
+  if (chk) {
+    if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
+    hipLaunchKernelGGL(lap_certify, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, mon, n,
+                       *chk, d_scores);
+  }
   if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
   if (trace) {
     std::vector<unsigned long long> h((size_t)g.blocks * LAP_TRACE_SLOTS);
@@ -1071,13 +1151,14 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
 
 int lap_launch(const LapGeom &g, bool f16, bool sop, const uint8_t *d_seqs,
                const int64_t *d_offsets, int32_t n, int32_t *d_scores, void *d_ws,
-               const PencilArgs &pa, hipStream_t stream, int32_t **d_err) {
+               const PencilArgs &pa, hipStream_t stream, int32_t **d_err,
+               const CheckLimits *chk) {
   if (d_err) {  // synchronous caller: clear the error word, it reads it back
     *d_err = (int32_t *)d_ws + (int64_t)n * g.G * g.GZ * LAP_PROG_STRIDE;
     if (hipMemsetAsync(*d_err, 0, sizeof(int32_t), stream) != hipSuccess) return TSA_EDEVICE;
   }
   return TSA_LAP_SHAPES(launch_lap, g.M, g.NW, f16, sop, d_seqs, d_offsets, n, g, d_scores, d_ws,
-                        pa, stream);
+                        pa, stream, chk);
 }
 
 }  // namespace tsa

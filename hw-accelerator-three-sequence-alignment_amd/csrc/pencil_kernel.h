@@ -23,14 +23,26 @@ bool pencil_shape_supported(int32_t max_la, int32_t max_lb, int32_t max_lc);
 //                   launch and rescore with LAP_OFF when it is set).
 // A lap launch that times out reports TSA_SCORE_INVALID for its triples.
 enum LapPolicy { LAP_OFF = 0, LAP_RESIDENT = 1, LAP_STREAM = 2 };
+// Certification limits of the checked kernel (DESIGN.md 1.2 with the observed
+// range of best in place of the a-priori one): a triple's scores stand when
+// max(best) <= best_max and min(best) >= best_min.
+struct CheckLimits {
+  int32_t best_max, best_min;
+};
 size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
-                              const KParams &kp, const Range &bound, LapPolicy lap);
+                              const KParams &kp, const Range &bound, LapPolicy lap,
+                              bool checked = false);
 // The plan pencil_launch_batch would run, as text (tsa_describe_plan).
 void pencil_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
-                     const Range &bound, LapPolicy lap, char *buf, size_t len);
+                     const Range &bound, LapPolicy lap, char *buf, size_t len, bool checked = false);
 int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                         int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
                         const Range &bound, int32_t *d_scores, void *d_ws, size_t ws_bytes,
-                        hipStream_t stream, LapPolicy lap, int32_t **d_err);
+                        hipStream_t stream, LapPolicy lap, int32_t **d_err,
+                        const CheckLimits *chk = nullptr);
+// The checked lap kernel (TSA_KERNEL_CHECKED) can run this batch: the lap
+// schedule is chosen for it (int16 arithmetic).
+bool pencil_checked_plan(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
+                         const KParams &kp, LapPolicy lap);
 
 }  // namespace tsa

@@ -139,7 +139,7 @@ static double helix_est(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_l
 // the rings are then full length (no producer ever waits for a consumer), the
 // waits are bounded and the caller checks the error word and falls back.
 static LapGeom lap_choice(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
-                          LapPolicy lap, bool f16, bool sop) {
+                          LapPolicy lap, bool f16, bool sop, bool need = false) {
   LapGeom none{};
   none.ok = false;
   if (lap == LAP_OFF || max_la > 4096 || max_la + 2 * 8 + 64 * 4 >= 8192) return none;
@@ -161,12 +161,23 @@ static LapGeom lap_choice(int32_t n, int32_t max_la, int32_t max_lb, int32_t max
       if (!best.ok || g.est_us < best.est_us) best = g;
     }
   }
-  if (best.ok && !force && best.est_us >= helix_est(n, max_la, max_lb, max_lc)) return none;
+  // `need` (the checked kernel): the lap schedule whatever the helix would cost
+  if (best.ok && !force && !need && best.est_us >= helix_est(n, max_la, max_lb, max_lc)) return none;
   return best;
 }
 
+bool pencil_checked_plan(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
+                         const KParams &kp, LapPolicy lap) {
+  return pencil_shape_ok(max_la, max_lb, max_lc) &&
+         lap_choice(n, max_la, max_lb, max_lc, lap, false, kp.s3_mode == TSA_S3_SOP, true).ok;
+}
+
 size_t pencil_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
-                              const KParams &kp, const Range &bound, LapPolicy lap) {
+                              const KParams &kp, const Range &bound, LapPolicy lap, bool checked) {
+  if (checked) {
+    const LapGeom g = lap_choice(n, max_la, max_lb, max_lc, lap, false, kp.s3_mode == TSA_S3_SOP, true);
+    return g.ok ? lap_workspace_bytes(g) : 0;
+  }
   if (!pencil_shape_ok(max_la, max_lb, max_lc)) return 0;
   const size_t helix = (size_t)std::min<int32_t>(n, 65535) *
                        (size_t)pencil_geom(max_la, max_lc).ring_bytes_per_triple;
@@ -700,14 +711,14 @@ static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
 }
 
 void pencil_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
-                     const Range &bound, LapPolicy lap, char *buf, size_t len) {
-  const bool f16 = use_f16(kp, bound);
+                     const Range &bound, LapPolicy lap, char *buf, size_t len, bool checked) {
+  const bool f16 = checked ? false : use_f16(kp, bound);
   const char *arith = f16 ? "f16" : "i16";
   const char *s3 = kp.s3_mode == TSA_S3_SOP ? "sop" : "rtl";
-  const LapGeom lg = lap_choice(n, max_la, max_lb, max_lc, lap, f16, kp.s3_mode == TSA_S3_SOP);
+  const LapGeom lg = lap_choice(n, max_la, max_lb, max_lc, lap, f16, kp.s3_mode == TSA_S3_SOP, checked);
   if (lg.ok) {
-    snprintf(buf, len, "pencil lap %s %s M=%d NW=%d laps=%d tiles=%d waves=%lld", arith, s3, lg.M,
-             lg.NW, lg.G, lg.GZ, (long long)lg.waves);
+    snprintf(buf, len, "pencil lap %s %s M=%d NW=%d laps=%d tiles=%d waves=%lld%s", arith, s3, lg.M,
+             lg.NW, lg.G, lg.GZ, (long long)lg.waves, checked ? " checked" : "");
     return;
   }
   const PencilGeom g = pencil_geom(max_la, max_lc);
@@ -718,18 +729,20 @@ void pencil_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, 
 int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                         int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
                         const Range &bound, int32_t *d_scores, void *d_ws, size_t ws_bytes,
-                        hipStream_t stream, LapPolicy lap, int32_t **d_err) {
+                        hipStream_t stream, LapPolicy lap, int32_t **d_err,
+                        const CheckLimits *chk) {
   if (d_err) *d_err = nullptr;
   if (n <= 0) return TSA_OK;
   if (!pencil_shape_ok(max_la, max_lb, max_lc)) return TSA_EINVAL;
-  const bool f16 = use_f16(kp, bound);
+  const bool f16 = chk ? false : use_f16(kp, bound);  // the checked kernel runs int16
   const PencilArgs pa = make_args(kp, f16);
   const bool sop = pa.sop != 0;
-  const LapGeom lg = lap_choice(n, max_la, max_lb, max_lc, lap, f16, sop);
+  const LapGeom lg = lap_choice(n, max_la, max_lb, max_lc, lap, f16, sop, chk != nullptr);
   if (lg.ok) {
     if (ws_bytes < lap_workspace_bytes(lg)) return TSA_ENOMEM;
-    return lap_launch(lg, f16, sop, d_seqs, d_offsets, n, d_scores, d_ws, pa, stream, d_err);
+    return lap_launch(lg, f16, sop, d_seqs, d_offsets, n, d_scores, d_ws, pa, stream, d_err, chk);
   }
+  if (chk) return TSA_ERANGE;  // no lap schedule for this batch
   const PencilGeom g = pencil_geom(max_la, max_lc);
   const int32_t grid = n < 65535 ? n : 65535;
   if (ws_bytes < (size_t)grid * (size_t)g.ring_bytes_per_triple) return TSA_ENOMEM;

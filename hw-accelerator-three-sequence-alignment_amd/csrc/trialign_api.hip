@@ -70,6 +70,28 @@ int build_kparams(const tsa_params *p, KParams *kp) {
   return TSA_OK;
 }
 
+// How far below the best of its predecessor a state (drop) and below a state
+// a candidate (cdrop) can sit: penalty minus the smallest score of the target.
+void bound_drops(const tsa_params *p, int64_t *drop, int64_t *cdrop) {
+  KParams kp;
+  build_kparams(p, &kp);
+  const int64_t m = p->match, mm = p->mismatch;
+  const int64_t s3min = p->s3_mode == TSA_S3_SOP ? std::min({3 * m, m + 2 * mm, 3 * mm})
+                                                 : std::min({3 * m, 2 * (m + mm), 3 * mm});
+  const int64_t s2min = std::min(m, mm);
+  *drop = 0;
+  *cdrop = 0;
+  for (int T = 0; T < 7; ++T) {
+    const int64_t scmin = T == SM ? s3min : T <= SIZ ? 0 : s2min;
+    int64_t maxp = kp.pen[T][0];
+    for (int s = 0; s < 7; ++s) {
+      maxp = std::max<int64_t>(maxp, kp.pen[T][s]);
+      *cdrop = std::max<int64_t>(*cdrop, kp.pen[T][s] - scmin);
+    }
+    *drop = std::max<int64_t>(*drop, maxp - scmin);
+  }
+}
+
 Range value_bound(const tsa_params *p, int64_t la, int64_t lb, int64_t lc) {
   KParams kp;
   build_kparams(p, &kp);
@@ -95,14 +117,7 @@ Range value_bound(const tsa_params *p, int64_t la, int64_t lb, int64_t lc) {
   const int64_t mn = std::min(la, std::min(lb, lc));
   const int64_t bestlo = mn * std::min<int64_t>(0, s3min);
   int64_t drop = 0, cdrop = 0;
-  for (int T = 0; T < 7; ++T) {
-    int64_t maxp = kp.pen[T][0];
-    for (int s = 0; s < 7; ++s) {
-      maxp = std::max<int64_t>(maxp, kp.pen[T][s]);
-      cdrop = std::max<int64_t>(cdrop, kp.pen[T][s] - scmin[T]);
-    }
-    drop = std::max<int64_t>(drop, maxp - scmin[T]);
-  }
+  bound_drops(p, &drop, &cdrop);
   const int64_t statelo = std::min<int64_t>(0, bestlo - drop);
   Range r;
   r.lo = statelo - std::max<int64_t>(0, cdrop);
@@ -183,11 +198,54 @@ static bool pencil_exact(const tsa_params *p, int64_t la, int64_t lb, int64_t lc
          pencil_shape_supported((int32_t)la, (int32_t)lb, (int32_t)lc);
 }
 
+// Can the checked kernel (TSA_KERNEL_CHECKED) score these lengths? The int16
+// carrier holds the a-priori bound (no wrap of its own), only the RTL's
+// SCORE_BITS wrap cannot be ruled out a priori.
+static bool pencil_checkable(const tsa_params *p, int64_t la, int64_t lb, int64_t lc) {
+  if (p->score_bits == 0 || !pencil_supported(p) ||
+      !pencil_shape_supported((int32_t)la, (int32_t)lb, (int32_t)lc))
+    return false;
+  const Range r = value_bound(p, la, lb, lc);
+  const int64_t slack = pencil_slack(p->match, p->mismatch, p->gap_open, p->gap_extend);
+  return r.lo - slack >= -32768 && r.hi + slack <= 32767;
+}
+
+// The checked kernel's certification (DESIGN.md 1.2 with the observed range
+// of best in place of the a-priori one): every state lies in
+// [min(0, bmin - drop), bmax] and every candidate above that minus cdrop, so
+// no candidate wraps at SCORE_BITS when bmax fits and bmin >= lo + drop + cdrop.
+static CheckLimits check_limits(const tsa_params *p) {
+  const int64_t lim_lo = -(1LL << (p->score_bits - 1)), lim_hi = (1LL << (p->score_bits - 1)) - 1;
+  int64_t drop = 0, cdrop = 0;
+  bound_drops(p, &drop, &cdrop);
+  CheckLimits c;
+  c.best_max = (int32_t)lim_hi;
+  c.best_min = -std::max<int64_t>(0, cdrop) < lim_lo ? INT32_MAX  // never certifiable
+                                                    : (int32_t)(lim_lo + drop + std::max<int64_t>(0, cdrop));
+  return c;
+}
+
+// TSA_KERNEL_CHECKED is an internal kind too: AUTO upgrades PLANE to it on the
+// synchronous paths (upgrade_checked).
 static int choose_kernel(int32_t kernel, const tsa_params *p, int64_t la, int64_t lb, int64_t lc) {
   if (kernel == TSA_KERNEL_PLANE) return TSA_KERNEL_PLANE;
   const bool ok = pencil_exact(p, la, lb, lc);
   if (kernel == TSA_KERNEL_PENCIL) return ok ? TSA_KERNEL_PENCIL : -1;
+  if (kernel == TSA_KERNEL_CHECKED)
+    return ok ? TSA_KERNEL_PENCIL : pencil_checkable(p, la, lb, lc) ? TSA_KERNEL_CHECKED : -1;
   return ok ? TSA_KERNEL_PENCIL : TSA_KERNEL_PLANE;
+}
+static bool checked_plan(int32_t n, const tsa_params *p, int32_t la, int32_t lb, int32_t lc,
+                         LapPolicy lap) {
+  KParams kp;
+  return build_kparams(p, &kp) == TSA_OK && pencil_checked_plan(std::min(n, 65535), la, lb, lc, kp, lap);
+}
+static int upgrade_checked(int kind, int32_t kernel, int32_t n, const tsa_params *p, int32_t la,
+                           int32_t lb, int32_t lc) {
+  if (kind == TSA_KERNEL_PLANE && kernel == TSA_KERNEL_AUTO && pencil_checkable(p, la, lb, lc) &&
+      checked_plan(n, p, la, lb, lc, LAP_STREAM))
+    return TSA_KERNEL_CHECKED;
+  return kind;
 }
 
 // lap: LAP_STREAM only on the synchronous paths, which check the lap kernel's
@@ -198,12 +256,14 @@ static size_t workspace_for(int kind, int32_t n, int32_t max_la, int32_t max_lb,
   KParams kp;
   if (build_kparams(p, &kp)) return 0;
   return pencil_workspace_bytes(n, max_la, max_lb, max_lc, kp, value_bound(p, max_la, max_lb, max_lc),
-                                lap);
+                                lap, kind == TSA_KERNEL_CHECKED);
 }
 
 // Lap hand-offs that timed out on the synchronous path (each rescored by the
 // helix kernel), process-wide; tsa_fallback_count() reads it.
 static std::atomic<int64_t> g_lap_fallbacks{0};
+// Triples the checked kernel could not certify (rescored by PLANE).
+static std::atomic<int64_t> g_check_fallbacks{0};
 
 static int launch_kind(int kind, const uint8_t *d_seqs, const int64_t *d_off, int32_t n,
                        int32_t max_la, int32_t max_lb, int32_t max_lc, const tsa_params *p,
@@ -215,9 +275,10 @@ static int launch_kind(int kind, const uint8_t *d_seqs, const int64_t *d_off, in
   if (kind == TSA_KERNEL_PLANE)
     return plane_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp, d_scores, d_final7,
                               ws, ws_bytes, s);
+  const CheckLimits lim = check_limits(p);
   return pencil_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp,
                              value_bound(p, max_la, max_lb, max_lc), d_scores, ws, ws_bytes, s,
-                             lap, d_err);
+                             lap, d_err, kind == TSA_KERNEL_CHECKED ? &lim : nullptr);
 }
 
 #define HIPCHK(x)                                   \
@@ -239,14 +300,17 @@ static int run_host_batch_on_device(int device, const uint8_t *seqs, const int64
     max_lb = std::max<int32_t>(max_lb, (int32_t)(o[2] - o[1]));
     max_lc = std::max<int32_t>(max_lc, (int32_t)(o[3] - o[2]));
   }
-  const int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
+  int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
   if (kind < 0) return TSA_ERANGE;
+  if (!final7) kind = upgrade_checked(kind, kernel, n, p, max_la, max_lb, max_lc);
   // chunk so the workspace stays under ~8 GiB and the grid under 65535
   // triples; the workspace is what the chunk's own plan (lap for a few cubes,
-  // the helix ring otherwise) and its helix fallback need
+  // the helix ring otherwise) and its fallback (helix; PLANE for the checked
+  // kernel) need
   auto ws_of = [&](int32_t c) {
     return std::max(workspace_for(kind, c, max_la, max_lb, max_lc, p, LAP_STREAM),
-                    workspace_for(kind, c, max_la, max_lb, max_lc, p, LAP_OFF));
+                    kind == TSA_KERNEL_CHECKED ? workspace_for(TSA_KERNEL_PLANE, c, max_la, max_lb, max_lc, p)
+                                               : workspace_for(kind, c, max_la, max_lb, max_lc, p, LAP_OFF));
   };
   const size_t cap = (size_t)8 << 30;
   int32_t chunk = std::min(n, 65535);
@@ -281,7 +345,23 @@ static int run_host_batch_on_device(int device, const uint8_t *seqs, const int64
     rc = launch_kind(kind, d_seqs, d_off + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p,
                      d_scores + c0, d_final ? d_final + 7 * (int64_t)c0 : nullptr, d_ws,
                      ws_bytes, s, LAP_STREAM, &d_err);
-    if (rc == TSA_OK && d_err) {  // lap kernel: a timed-out hand-off invalidates the chunk
+    if (rc == TSA_OK && kind == TSA_KERNEL_CHECKED) {
+      // certified scores stand; a chunk with any other (uncertified, or a
+      // timed-out hand-off) is rescored by the literal PLANE kernel
+      int32_t herr = 0;
+      std::vector<int32_t> hs((size_t)cn);
+      HIPCHK(hipMemcpyAsync(&herr, d_err, sizeof(herr), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(hs.data(), d_scores + c0, (size_t)cn * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      int64_t bad = 0;
+      for (int32_t v : hs) bad += v == TSA_SCORE_UNCERTIFIED || v == TSA_SCORE_INVALID;
+      if (herr || bad) {
+        g_check_fallbacks.fetch_add(herr ? cn : bad);
+        if (herr) g_lap_fallbacks.fetch_add(1);
+        rc = launch_kind(TSA_KERNEL_PLANE, d_seqs, d_off + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc,
+                         p, d_scores + c0, nullptr, d_ws, ws_bytes, s);
+      }
+    } else if (rc == TSA_OK && d_err) {  // lap kernel: a timed-out hand-off invalidates the chunk
       int32_t herr = 0;
       HIPCHK(hipMemcpyAsync(&herr, d_err, sizeof(herr), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
@@ -322,7 +402,7 @@ int tsa_score_gpu_ex(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
                      int32_t lc, const tsa_params *p, int32_t kernel, int32_t *score,
                      int32_t *final_states, int32_t device) {
   if (!score) return TSA_EINVAL;
-  if (kernel < TSA_KERNEL_AUTO || kernel > TSA_KERNEL_PENCIL) return TSA_EINVAL;
+  if (kernel < TSA_KERNEL_AUTO || kernel > TSA_KERNEL_CHECKED) return TSA_EINVAL;
   int rc = tsa_validate(a, la, b, lb, c, lc, p);
   if (rc) return rc;
   const int nd = tsa_device_count();
@@ -338,6 +418,7 @@ int tsa_score_gpu_ex(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
 }
 
 int64_t tsa_fallback_count(void) { return g_lap_fallbacks.load(); }
+int64_t tsa_check_fallback_count(void) { return g_check_fallbacks.load(); }
 
 int tsa_score_gpu(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb, const uint8_t *c,
                   int32_t lc, const tsa_params *p, int32_t *score, int32_t device) {
@@ -445,26 +526,30 @@ int tsa_describe_plan(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
                       const tsa_params *p, int32_t kernel, int32_t sync, char *buf, size_t len) {
   if (!buf || len == 0 || n < 1 || max_la < 1 || max_lb < 1 || max_lc < 1 || !params_ok(p))
     return TSA_EINVAL;
-  const int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
+  int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
   if (kind < 0) return TSA_ERANGE;
+  if (sync) kind = upgrade_checked(kind, kernel, n, p, max_la, max_lb, max_lc);
   if (kind == TSA_KERNEL_PLANE) {
     snprintf(buf, len, "plane");
     return TSA_OK;
   }
+  const LapPolicy lap = sync ? LAP_STREAM : LAP_RESIDENT;
+  if (kind == TSA_KERNEL_CHECKED && !checked_plan(n, p, max_la, max_lb, max_lc, lap)) return TSA_ERANGE;
   KParams kp;
   build_kparams(p, &kp);
   pencil_describe(std::min(n, 65535), max_la, max_lb, max_lc, kp,
-                  value_bound(p, max_la, max_lb, max_lc), sync ? LAP_STREAM : LAP_RESIDENT, buf,
-                  len);
+                  value_bound(p, max_la, max_lb, max_lc), lap, buf, len, kind == TSA_KERNEL_CHECKED);
   return TSA_OK;
 }
 
 int tsa_batch_workspace_size(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
                              const tsa_params *p, int32_t kernel, size_t *bytes) {
   if (!bytes || n < 0 || max_la < 1 || max_lb < 1 || max_lc < 1 || !params_ok(p)) return TSA_EINVAL;
-  if (kernel < TSA_KERNEL_AUTO || kernel > TSA_KERNEL_PENCIL) return TSA_EINVAL;
+  if (kernel < TSA_KERNEL_AUTO || kernel > TSA_KERNEL_CHECKED) return TSA_EINVAL;
   const int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
   if (kind < 0) return TSA_ERANGE;
+  if (kind == TSA_KERNEL_CHECKED && !checked_plan(n, p, max_la, max_lb, max_lc, LAP_RESIDENT))
+    return TSA_ERANGE;
   *bytes = workspace_for(kind, n, max_la, max_lb, max_lc, p);
   return TSA_OK;
 }
@@ -476,7 +561,7 @@ int tsa_score_batch_async(const uint8_t *d_seqs, const int64_t *d_offsets, int32
   if (!d_seqs || !d_offsets || !d_scores || !d_workspace || n < 0 || max_la < 1 || max_lb < 1 ||
       max_lc < 1 || !params_ok(p))
     return TSA_EINVAL;
-  if (kernel < TSA_KERNEL_AUTO || kernel > TSA_KERNEL_PENCIL) return TSA_EINVAL;
+  if (kernel < TSA_KERNEL_AUTO || kernel > TSA_KERNEL_CHECKED) return TSA_EINVAL;
   if (tsa_device_count() <= 0) return TSA_ENODEV;
   if (p->score_bits == 0) {
     const Range r = value_bound(p, max_la, max_lb, max_lc);
@@ -484,6 +569,8 @@ int tsa_score_batch_async(const uint8_t *d_seqs, const int64_t *d_offsets, int32
   }
   const int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
   if (kind < 0) return TSA_ERANGE;
+  if (kind == TSA_KERNEL_CHECKED && !checked_plan(n, p, max_la, max_lb, max_lc, LAP_RESIDENT))
+    return TSA_ERANGE;
   if (workspace_bytes < workspace_for(kind, n, max_la, max_lb, max_lc, p)) return TSA_ENOMEM;
   hipStream_t s = (hipStream_t)stream;
   for (int32_t c0 = 0; c0 < n; c0 += 65535) {

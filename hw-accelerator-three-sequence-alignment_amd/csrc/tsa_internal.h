@@ -35,6 +35,9 @@ struct Range {
 
 int build_kparams(const tsa_params *p, KParams *kp);
 Range value_bound(const tsa_params *p, int64_t la, int64_t lb, int64_t lc);
+// How far a state can sit below its best predecessor (drop) and a candidate
+// below a state (cdrop), for value_bound and the checked kernel.
+void bound_drops(const tsa_params *p, int64_t *drop, int64_t *cdrop);
 
 // Row stride (elements) of a (y,z) plane with lc+1 columns, padded so rows
 // start 16-byte aligned for int16 storage.

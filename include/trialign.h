@@ -62,6 +62,12 @@ extern "C" {
  * rescore such triples themselves (tsa_fallback_count counts it). */
 #define TSA_SCORE_INVALID INT32_MIN
 
+/* Score reported by TSA_KERNEL_CHECKED for a triple whose values may have
+ * left the SCORE_BITS range (so the RTL's wrapped result may differ): rescore
+ * it with TSA_KERNEL_PLANE. The synchronous entry points do that themselves
+ * (tsa_check_fallback_count counts it). */
+#define TSA_SCORE_UNCERTIFIED (INT32_MIN + 1)
+
 #define TSA_S3_RTL 0 /* temp_ABC as the RTL evaluates it (src/PE_1cyc.v:162) */
 #define TSA_S3_SOP 1 /* sum of the three pair scores                          */
 
@@ -69,6 +75,16 @@ extern "C" {
 #define TSA_KERNEL_AUTO 0
 #define TSA_KERNEL_PLANE 1  /* anti-diagonal plane sweep, literal RTL arithmetic */
 #define TSA_KERNEL_PENCIL 2 /* register-systolic pencil sweep (factored form)    */
+/* The pencil lap kernel in int16 with a range monitor, for cubes whose a-priori
+ * bound exceeds SCORE_BITS (beyond ~680 per side with the RTL constants) but
+ * whose values may well stay inside it: the factored form is exact whenever
+ * no value of the literal recurrence wraps, and the monitor proves that per
+ * triple (every real cell's best, then the candidate bound of DESIGN.md 1.2)
+ * or reports TSA_SCORE_UNCERTIFIED. TSA_KERNEL_AUTO uses it on the
+ * synchronous entry points (rescoring uncertified triples with PLANE); the
+ * async path only runs it when asked. Single cubes / small batches (the lap
+ * schedule) only: TSA_ERANGE otherwise. */
+#define TSA_KERNEL_CHECKED 3
 
 typedef struct tsa_params {
   int32_t match;      /* MATCH      (src/PE_1cyc.v:55), default  1 */
@@ -167,6 +183,10 @@ int tsa_describe_plan(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
  * the library was loaded; each was rescored with the helix kernel (and logged
  * to stderr). 0 in a healthy run. */
 int64_t tsa_fallback_count(void);
+
+/* Triples the checked kernel could not certify on the synchronous entry points
+ * since the library was loaded; each was rescored with the PLANE kernel. */
+int64_t tsa_check_fallback_count(void);
 
 /* Number of visible HIP devices (0 when none), or a negative code. */
 int tsa_device_count(void);

@@ -111,8 +111,17 @@ def test_describe_plan(tsa):
     with pytest.raises(tsa.TsaError) as e:
         tsa.describe_plan(4, 64, 64, 64, ge, kernel="pencil")
     assert e.value.rc == tsa.TSA_ERANGE
-    # wrapping parameter sets stay on the literal plane kernel
-    assert tsa.describe_plan(4, 90, 90, 90, tsa.TsaParams.default(score_bits=6)) == "plane"
+    # parameter sets that may wrap: the literal plane kernel on the async path;
+    # the synchronous path tries the checked lap kernel first (PLANE rescoring
+    # whatever it cannot certify), and so does an explicit kernel="checked"
+    p6 = tsa.TsaParams.default(score_bits=6)
+    assert tsa.describe_plan(4, 90, 90, 90, p6, sync=False) == "plane"
+    assert tsa.describe_plan(4, 90, 90, 90, p6, sync=True).endswith(" checked")
+    assert tsa.describe_plan(1, 1024, 1024, 1024, p, sync=True).startswith("pencil lap i16 rtl")
+    assert tsa.describe_plan(1, 1024, 1024, 1024, p, sync=False) == "plane"
+    assert tsa.describe_plan(1, 1024, 1024, 1024, p, kernel="checked", sync=False).endswith(" checked")
+    # a batch too large for the lap schedule is never checked
+    assert tsa.describe_plan(4096, 800, 800, 800, p, sync=True) == "plane"
 
 
 @pytest.mark.skipif(os.environ.get("TSA_EXPECT_GPU") == "1", reason="GPU box")

@@ -467,3 +467,70 @@ def test_lap_kernel_geometries_adversarial(gpu, orc, monkeypatch, m, nw):
             else:
                 a, b, c = (rng.integers(0, 4, n).astype(np.uint8) for n in (la, lb, lc))
             assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (m, nw, la, lb, lc, kind)
+
+
+def _score_async(gpu, triples, p, kernel, L):
+    import torch
+    seqs, offs = gpu.pack_batch(triples)
+    n = len(triples)
+    d_seqs, d_offs = torch.from_numpy(seqs).cuda(), torch.from_numpy(offs).cuda()
+    d_score = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ws = gpu.workspace_size(n, L, L, L, p, kernel)
+    d_ws = torch.empty(max(ws, 16), dtype=torch.uint8, device="cuda")
+    gpu.score_batch_async(d_seqs.data_ptr(), d_offs.data_ptr(), n, L, L, L, d_score.data_ptr(),
+                          d_ws.data_ptr(), ws, torch.cuda.current_stream().cuda_stream, p, kernel)
+    torch.cuda.synchronize()
+    return d_score.cpu().numpy()
+
+
+def test_checked_1024_rtl_words(gpu, orc, synth):
+    """The RTL's 12-bit words at 1024^3 (a-priori bound 3072: the factored form
+    is not provably exact, round 1 ran 29 ms of PLANE): the checked lap kernel
+    monitors every real cell's best and certifies the random cube, so the
+    synchronous path returns the literal wrapped recurrence's score without a
+    PLANE rescore. Oracle: ~30 s of one core."""
+    L = 1024
+    a, b, c = synth.triple(5, L)
+    p = gpu.TsaParams.default()
+    assert gpu.describe_plan(1, L, L, L, p, sync=True).endswith(" checked")
+    before = gpu.check_fallback_count()
+    got = gpu.score(a, b, c, p)
+    assert got == orc.score(a, b, c, orc.default_params())
+    assert gpu.check_fallback_count() == before
+    assert _score_async(gpu, [(a, b, c)], p, "checked", L)[0] == got
+
+
+@pytest.mark.parametrize("kind", ["match", "mismatch"])
+def test_checked_uncertified_falls_back_to_plane(gpu, orc, kind):
+    """Cubes whose values do leave the word: all-match 690^3 with 12-bit words
+    (score 2070 wraps), all-mismatch 90^3 with 8-bit words (best down to -180).
+    The monitor refuses to certify: async reports TSA_SCORE_UNCERTIFIED, the
+    synchronous path rescored with PLANE (counted) and returns the RTL's
+    wrapped score. (All-mismatch with 12-bit words does not wrap -- its best
+    stays near -2 per position -- and is certified: see the 1024^3 test.)"""
+    if kind == "match":
+        L, bits = 690, 12
+        a = b = c = np.zeros(L, np.uint8)
+    else:
+        L, bits = 90, 8
+        a, b, c = (np.full(L, v, np.uint8) for v in (0, 1, 2))
+    p, op = gpu.TsaParams.default(score_bits=bits), orc.default_params(score_bits=bits)
+    ref = orc.score(a, b, c, op)
+    assert _score_async(gpu, [(a, b, c)], p, "checked", L)[0] == gpu.SCORE_UNCERTIFIED
+    before = gpu.check_fallback_count()
+    assert gpu.score(a, b, c, p) == ref
+    assert gpu.check_fallback_count() == before + 1
+
+
+def test_checked_narrow_words_batch(gpu, orc):
+    """SCORE_BITS 8 and 9 on small cubes: the synchronous batch path tries the
+    checked kernel, certifies what stays in range and rescores the rest with
+    PLANE -- every score equals the literal wrapped oracle."""
+    rng = np.random.default_rng(91)
+    for bits in (8, 9):
+        triples = [tuple(rng.integers(0, 4, n).astype(np.uint8) for n in (90, 70, 100))
+                   for _ in range(3)]
+        p, op = gpu.TsaParams.default(score_bits=bits), orc.default_params(score_bits=bits)
+        assert gpu.describe_plan(3, 90, 70, 100, p, sync=True).endswith(" checked")
+        seqs, offs = gpu.pack_batch(triples)
+        assert np.array_equal(gpu.score_batch(triples, p), orc.score_batch(seqs, offs, op, nthreads=3))

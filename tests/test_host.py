@@ -70,10 +70,12 @@ def test_pencil_exact_dispatch_bounds(tsa):
     """pencil_exact: the 12-bit RTL wrap is checked against the bare value
     bound and the carrier against the bound plus a few penalties -- pencil up
     to 680 per side with 12-bit words, exact f16 up to ~676, the literal plane
-    kernel beyond."""
+    kernel beyond (async), the checked lap kernel beyond (synchronous)."""
     for L, want in [(256, "pencil"), (512, "pencil"), (600, "pencil"), (680, "pencil"),
                     (681, "plane"), (1024, "plane")]:
-        assert tsa.describe_plan(1, L, L, L).split()[0] == want, L
+        assert tsa.describe_plan(1, L, L, L, sync=False).split()[0] == want, L
+        checked = tsa.describe_plan(1, L, L, L, sync=True).endswith(" checked")
+        assert checked == (want == "plane"), L
     assert " f16 " in tsa.describe_plan(1, 512, 512, 512)
     assert " i16 " in tsa.describe_plan(1, 680, 680, 680)
 
