@@ -62,7 +62,7 @@ EXPORTS = (
     "tsa_default_params", "tsa_validate", "tsa_score_gpu", "tsa_score_gpu_ex",
     "tsa_score_batch", "tsa_batch_workspace_size", "tsa_score_batch_async",
     "tsa_device_count", "tsa_strerror", "tsa_version", "tsa_describe_plan", "tsa_align_gpu",
-    "tsa_fallback_count", "tsa_check_fallback_count",
+    "tsa_fallback_count", "tsa_check_fallback_count", "tsa_score_batch_async_p2", "tsa_pack2",
 )
 
 # Score of a triple the device could not score (include/trialign.h).
@@ -138,6 +138,8 @@ def _load_lib() -> ctypes.CDLL:
                                   pp, i32p, u8p, ctypes.c_int32, i32p, i32p, ctypes.c_int32]
     lib.tsa_fallback_count.argtypes = []
     lib.tsa_fallback_count.restype = ctypes.c_int64
+    lib.tsa_score_batch_async_p2.argtypes = lib.tsa_score_batch_async.argtypes
+    lib.tsa_pack2.argtypes = [u8p, ctypes.c_int64, u8p]
     lib.tsa_check_fallback_count.argtypes = []
     lib.tsa_check_fallback_count.restype = ctypes.c_int64
     lib.tsa_device_count.argtypes = []
@@ -147,7 +149,7 @@ def _load_lib() -> ctypes.CDLL:
     lib.tsa_version.restype = ctypes.c_char_p
     for name in ("tsa_validate", "tsa_score_gpu", "tsa_score_gpu_ex", "tsa_score_batch",
                  "tsa_batch_workspace_size", "tsa_score_batch_async", "tsa_device_count",
-                 "tsa_describe_plan", "tsa_align_gpu"):
+                 "tsa_describe_plan", "tsa_align_gpu", "tsa_score_batch_async_p2", "tsa_pack2"):
         getattr(lib, name).restype = ctypes.c_int
     return lib
 
@@ -379,6 +381,31 @@ def score_batch_async(d_seqs_ptr: int, d_offsets_ptr: int, n: int, max_la: int, 
                                     ctypes.c_void_p(d_scores_ptr), ctypes.c_void_p(d_ws_ptr),
                                     ctypes.c_size_t(ws_bytes), ctypes.c_void_p(stream_ptr))
     _check(rc, "tsa_score_batch_async")
+
+
+def pack2(seqs) -> np.ndarray:
+    """Symbols (0..4) -> 2-bit packed bytes, four per byte, symbol i at bits
+    2(i%4) of byte i/4 (tsa_pack2; N = 4 packs as A, as the RTL's 2-bit
+    registers hold it)."""
+    s = np.ascontiguousarray(_as_u8(seqs) if not isinstance(seqs, np.ndarray) else seqs, dtype=np.uint8)
+    out = np.zeros(max((len(s) + 3) // 4, 1), dtype=np.uint8)
+    _check(_lib.tsa_pack2(_ptr(s, ctypes.c_uint8), len(s), _ptr(out, ctypes.c_uint8)), "tsa_pack2")
+    return out[: (len(s) + 3) // 4]
+
+
+def score_batch_async_p2(d_packed_ptr: int, d_offsets_ptr: int, n: int, max_la: int, max_lb: int,
+                         max_lc: int, d_scores_ptr: int, d_ws_ptr: int, ws_bytes: int,
+                         stream_ptr: int = 0, params: Optional[TsaParams] = None,
+                         kernel: str | int = "auto") -> None:
+    """score_batch_async on 2-bit packed sequences (tsa_score_batch_async_p2):
+    d_packed holds pack2(seqs), offsets still count symbols."""
+    p = params or TsaParams.default()
+    k = KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
+    rc = _lib.tsa_score_batch_async_p2(ctypes.c_void_p(d_packed_ptr), ctypes.c_void_p(d_offsets_ptr),
+                                       n, max_la, max_lb, max_lc, ctypes.byref(p), k,
+                                       ctypes.c_void_p(d_scores_ptr), ctypes.c_void_p(d_ws_ptr),
+                                       ctypes.c_size_t(ws_bytes), ctypes.c_void_p(stream_ptr))
+    _check(rc, "tsa_score_batch_async_p2")
 
 
 # ---- the testbench's sequence RAM image (src/TriAlign_tb.sv:94-96,149-169) ----

@@ -416,8 +416,8 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
   const int32_t na = la + 2 * ZT + 4 * NW + 8;
   for (int j = threadIdx.x; j < na; j += 64 * (NW + 1)) {
     const int x0 = j - OFF, x1 = j - OFF - 1;
-    const uint32_t c0 = (x0 >= 0 && x0 < la) ? SYM0 << (seqs[o0 + x0] & 3) : 0u;
-    const uint32_t c1 = (x1 >= 0 && x1 < la) ? SYM0 << (seqs[o0 + x1] & 3) : 0u;
+    const uint32_t c0 = (x0 >= 0 && x0 < la) ? SYM0 << tsa_sym(seqs, o0 + x0, pa.packed) : 0u;
+    const uint32_t c1 = (x1 >= 0 && x1 < la) ? SYM0 << tsa_sym(seqs, o0 + x1, pa.packed) : 0u;
     sA2[j] = c0 | (c1 << 16);
   }
   if (threadIdx.x < 16) wd[threadIdx.x] = 0;
@@ -576,8 +576,8 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
     const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
                             4u * (uint32_t)(OFF - 2 * w - M * lane - (M - 1));
     const int32_t y0 = L * RW + 2 * w;  // rows y0 (lo) and y0 + 1 (hi), 0-based
-    const uint32_t bw = (y0 < lb ? SYM0 << (seqs[o1 + y0] & 3) : 0u) |
-                        ((y0 + 1 < lb ? SYM0 << (seqs[o1 + y0 + 1] & 3) : 0u) << 16);
+    const uint32_t bw = (y0 < lb ? SYM0 << tsa_sym(seqs, o1 + y0, pa.packed) : 0u) |
+                        ((y0 + 1 < lb ? SYM0 << tsa_sym(seqs, o1 + y0 + 1, pa.packed) : 0u) << 16);
     uint32_t bv[M], c[M], SBC[M], K_[M], DMC[M];
     uint32_t oIx[M], shIz[M], svIxy[M], svIyz[M], shIxz[2][M], svM[2][M];
     uint32_t pIy[M], pIxy[M], pIyz[M], pBest[M];  // this wave's record of the previous step
@@ -588,7 +588,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         const int k = M * lane + i;
-        c[i] = (k < zt_q ? SYM0 << (seqs[oc + k] & 3) : 0u) * 0x00010001u;
+        c[i] = (k < zt_q ? SYM0 << tsa_sym(seqs, oc + k, pa.packed) : 0u) * 0x00010001u;
         DMC[i] = dm_over_code(pa.dmf, c[i]);
         bv[i] = bw;
         const uint32_t e01 = pk_eq1(bw, c[i], one1);

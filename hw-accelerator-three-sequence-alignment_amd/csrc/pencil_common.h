@@ -67,6 +67,7 @@ struct PencilArgs {
   uint32_t h_sbc, h_k0, h_kd;     // per-row registers, see cell_messages_f16
   float dmf;                      // match - mismatch (per-position DMC, exact f16)
   int32_t sop;                  // TSA_S3_SOP
+  int32_t packed;               // 2-bit packed input symbols (tsa_sym)
 };
 
 

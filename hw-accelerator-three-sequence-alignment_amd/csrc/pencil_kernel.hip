@@ -258,16 +258,16 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     // B; face records in the ring
     for (int j = threadIdx.x; j < P + ZT; j += 64 * NW) {
       const int x0 = ((j - ZT) % P + P) % P, x1 = TWO ? x0 : ((j - ZT - 64 * M) % P + P) % P;
-      const uint32_t c0 = x0 < la ? SYM0 << (seqs[o0 + x0] & 3) : 0u;
-      const uint32_t c1 = x1 < la1 ? SYM0 << (seqs[(TWO ? q0 : o0) + x1] & 3) : 0u;
+      const uint32_t c0 = x0 < la ? SYM0 << tsa_sym(seqs, o0 + x0, pa.packed) : 0u;
+      const uint32_t c1 = x1 < la1 ? SYM0 << tsa_sym(seqs, (TWO ? q0 : o0) + x1, pa.packed) : 0u;
       sA2[j] = c0 | (c1 << 16);
     }
     for (int i = threadIdx.x; i < lbm; i += 64 * NW) {
       if constexpr (TWO)
-        sB[i] = (i < lb ? SYM0 << (seqs[o1 + i] & 3) : 0u) |
-                ((i < lb1 ? SYM0 << (seqs[q1 + i] & 3) : 0u) << 16);
+        sB[i] = (i < lb ? SYM0 << tsa_sym(seqs, o1 + i, pa.packed) : 0u) |
+                ((i < lb1 ? SYM0 << tsa_sym(seqs, q1 + i, pa.packed) : 0u) << 16);
       else
-        sB[i] = (SYM0 << (seqs[o1 + i] & 3)) * 0x00010001u;
+        sB[i] = (SYM0 << tsa_sym(seqs, o1 + i, pa.packed)) * 0x00010001u;
     }
     {
       const uint4 face = make_uint4(pa.f_single, pa.f_pair, pa.f_pair, 0u);
@@ -283,8 +283,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll
     for (int i = 0; i < M; ++i) {
       const int k0 = M * lane + i, k1 = TWO ? k0 : 64 * M + M * lane + i;
-      const uint32_t c0 = k0 < lc ? SYM0 << (seqs[o2 + k0] & 3) : 0u;
-      const uint32_t c1 = k1 < lc1 ? SYM0 << (seqs[(TWO ? q2 : o2) + k1] & 3) : 0u;
+      const uint32_t c0 = k0 < lc ? SYM0 << tsa_sym(seqs, o2 + k0, pa.packed) : 0u;
+      const uint32_t c1 = k1 < lc1 ? SYM0 << tsa_sym(seqs, (TWO ? q2 : o2) + k1, pa.packed) : 0u;
       c[i] = c0 | (c1 << 16);
       DMC[i] = dm_over_code(pa.dmf, c[i]);
       b[i] = SBC[i] = K[i] = 0;  // set when a position reaches x = 1 of its lap
@@ -629,6 +629,7 @@ PencilArgs make_args(const KParams &kp, bool f16) {
   PencilArgs a;
   memset(&a, 0, sizeof(a));
   a.sop = kp.s3_mode == TSA_S3_SOP;
+  a.packed = kp.packed;
   if (!f16) {
     a.E = pk16(GE);
     a.O = pk16(GO);

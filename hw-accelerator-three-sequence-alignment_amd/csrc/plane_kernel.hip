@@ -130,7 +130,8 @@ __global__ __launch_bounds__(256) void plane_step_kernel(
     pYZ[s] = q2[s * P + cmm];  // (x,  y-1,z-1)  Iyz  :204-210
     pXZ[s] = q2[s * P + c0m];  // (x-1,y,  z-1)  Ixz  :212-218
   }
-  const int a = seqs[o0 + x - 1] & 3, b = seqs[o1 + y - 1] & 3, c = seqs[o2 + z - 1] & 3;
+  const int a = tsa_sym(seqs, o0 + x - 1, kp.packed), b = tsa_sym(seqs, o1 + y - 1, kp.packed),
+            c = tsa_sym(seqs, o2 + z - 1, kp.packed);
   const int32_t sh = kp.wrap_shift;
   const int32_t sab = (a == b) ? kp.match : kp.mismatch;
   const int32_t sbc = (b == c) ? kp.match : kp.mismatch;

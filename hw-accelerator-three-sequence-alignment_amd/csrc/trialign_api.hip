@@ -268,10 +268,12 @@ static std::atomic<int64_t> g_check_fallbacks{0};
 static int launch_kind(int kind, const uint8_t *d_seqs, const int64_t *d_off, int32_t n,
                        int32_t max_la, int32_t max_lb, int32_t max_lc, const tsa_params *p,
                        int32_t *d_scores, int32_t *d_final7, void *ws, size_t ws_bytes,
-                       hipStream_t s, LapPolicy lap = LAP_RESIDENT, int32_t **d_err = nullptr) {
+                       hipStream_t s, LapPolicy lap = LAP_RESIDENT, int32_t **d_err = nullptr,
+                       int32_t packed = 0) {
   KParams kp;
   int rc = build_kparams(p, &kp);
   if (rc) return rc;
+  kp.packed = packed;
   if (kind == TSA_KERNEL_PLANE)
     return plane_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp, d_scores, d_final7,
                               ws, ws_bytes, s);
@@ -554,10 +556,12 @@ int tsa_batch_workspace_size(int32_t n, int32_t max_la, int32_t max_lb, int32_t 
   return TSA_OK;
 }
 
-int tsa_score_batch_async(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
-                          int32_t max_la, int32_t max_lb, int32_t max_lc, const tsa_params *p,
-                          int32_t kernel, int32_t *d_scores, void *d_workspace,
-                          size_t workspace_bytes, void *stream) {
+}  // extern "C"
+
+static int score_batch_async(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
+                             int32_t max_la, int32_t max_lb, int32_t max_lc, const tsa_params *p,
+                             int32_t kernel, int32_t *d_scores, void *d_workspace,
+                             size_t workspace_bytes, void *stream, int32_t packed) {
   if (!d_seqs || !d_offsets || !d_scores || !d_workspace || n < 0 || max_la < 1 || max_lb < 1 ||
       max_lc < 1 || !params_ok(p))
     return TSA_EINVAL;
@@ -577,8 +581,39 @@ int tsa_score_batch_async(const uint8_t *d_seqs, const int64_t *d_offsets, int32
     const int32_t cn = std::min<int32_t>(65535, n - c0);
     const size_t wsz = workspace_for(kind, cn, max_la, max_lb, max_lc, p);
     int rc = launch_kind(kind, d_seqs, d_offsets + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p,
-                         d_scores + c0, nullptr, d_workspace, wsz, s);
+                         d_scores + c0, nullptr, d_workspace, wsz, s, LAP_RESIDENT, nullptr, packed);
     if (rc) return rc;
+  }
+  return TSA_OK;
+}
+
+extern "C" {
+
+int tsa_score_batch_async(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
+                          int32_t max_la, int32_t max_lb, int32_t max_lc, const tsa_params *p,
+                          int32_t kernel, int32_t *d_scores, void *d_workspace,
+                          size_t workspace_bytes, void *stream) {
+  return score_batch_async(d_seqs, d_offsets, n, max_la, max_lb, max_lc, p, kernel, d_scores,
+                           d_workspace, workspace_bytes, stream, 0);
+}
+
+int tsa_score_batch_async_p2(const uint8_t *d_packed, const int64_t *d_offsets, int32_t n,
+                             int32_t max_la, int32_t max_lb, int32_t max_lc, const tsa_params *p,
+                             int32_t kernel, int32_t *d_scores, void *d_workspace,
+                             size_t workspace_bytes, void *stream) {
+  return score_batch_async(d_packed, d_offsets, n, max_la, max_lb, max_lc, p, kernel, d_scores,
+                           d_workspace, workspace_bytes, stream, 1);
+}
+
+int tsa_pack2(const uint8_t *syms, int64_t n, uint8_t *out) {
+  if ((!syms || !out) && n > 0) return TSA_EINVAL;
+  if (n < 0) return TSA_EINVAL;
+  for (int64_t i = 0; i < n; ++i)
+    if (syms[i] > 4) return TSA_EINVAL;
+  for (int64_t j = 0; j < (n + 3) / 4; ++j) {
+    uint8_t v = 0;
+    for (int k = 0; k < 4 && 4 * j + k < n; ++k) v |= (uint8_t)((syms[4 * j + k] & 3) << (2 * k));
+    out[j] = v;
   }
   return TSA_OK;
 }

@@ -24,7 +24,15 @@ struct KParams {
   int32_t s3_mode;        // TSA_S3_RTL / TSA_S3_SOP
   int32_t bits;           // SCORE_BITS wrap, 0 = none
   int32_t wrap_shift;     // 32 - bits, or 0 when bits == 0
+  int32_t packed;         // input symbols 2-bit packed (tsa_score_batch_async_p2)
 };
+
+// Symbol i of a sequence buffer: one byte per symbol, or 2-bit packed (four
+// per byte, symbol i at bits 2(i%4) of byte i/4). Either way reduced mod 4,
+// as the PE's 2-bit symbol registers do (src/PE_1cyc.v:63-66).
+__device__ __forceinline__ uint32_t tsa_sym(const uint8_t *s, int64_t i, int32_t packed) {
+  return packed ? (uint32_t)(s[i >> 2] >> (2 * (i & 3))) & 3u : (uint32_t)s[i] & 3u;
+}
 
 // Inclusive bounds on every candidate and state value of a (la,lb,lc) cube
 // under params p (no wrap). Used to decide whether int16 storage and the

@@ -144,6 +144,20 @@ int tsa_score_batch_async(const uint8_t *d_seqs, const int64_t *d_offsets,
                           int32_t *d_scores, void *d_workspace,
                           size_t workspace_bytes, void *stream);
 
+/* tsa_score_batch_async on 2-bit packed sequences: d_packed holds symbol i of
+ * the batch buffer at bits [2(i%4)+1 : 2(i%4)] of byte i/4 (tsa_pack2);
+ * offsets count symbols, as above. The RTL keeps symbols in 2-bit registers
+ * (src/PE_1cyc.v:63-66: N = 4 scores as A), so packing loses nothing; the
+ * input is a quarter of the bytes. Same kernels, workspace and semantics. */
+int tsa_score_batch_async_p2(const uint8_t *d_packed, const int64_t *d_offsets,
+                             int32_t n, int32_t max_la, int32_t max_lb,
+                             int32_t max_lc, const tsa_params *p, int32_t kernel,
+                             int32_t *d_scores, void *d_workspace,
+                             size_t workspace_bytes, void *stream);
+/* Pack n symbols (0..4) four to a byte for tsa_score_batch_async_p2; out must
+ * hold (n + 3) / 4 bytes. TSA_EINVAL on a symbol above 4. Host only. */
+int tsa_pack2(const uint8_t *syms, int64_t n, uint8_t *out);
+
 /* Optimal alignment of one triple (synchronous, HIP device `device`): the
  * path behind the score, as one move per alignment column. This has no RTL
  * counterpart -- the testbench's alignment-output ports are commented out

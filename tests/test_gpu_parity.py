@@ -534,3 +534,33 @@ def test_checked_narrow_words_batch(gpu, orc):
         assert gpu.describe_plan(3, 90, 70, 100, p, sync=True).endswith(" checked")
         seqs, offs = gpu.pack_batch(triples)
         assert np.array_equal(gpu.score_batch(triples, p), orc.score_batch(seqs, offs, op, nthreads=3))
+
+
+@pytest.mark.parametrize("kernel", ["plane", "pencil", "auto"])
+def test_packed2_input_matches_bytes(gpu, orc, kernel):
+    """tsa_score_batch_async_p2: the same batch, 2-bit packed (ragged lengths,
+    so triples start mid-byte; N symbols), scores identically to the
+    byte-per-symbol input on every kernel family -- helix (batch), lap (a few
+    cubes) and plane -- and to the oracle."""
+    import torch
+    rng = np.random.default_rng(33)
+    for n, L in ((37, 70), (2, 200)):
+        triples = [tuple(rng.integers(0, 5, int(rng.integers(1, L + 1))).astype(np.uint8) for _ in range(3))
+                   for _ in range(n)]
+        seqs, offs = gpu.pack_batch(triples)
+        ml = [max(len(t[k]) for t in triples) for k in range(3)]
+        p = gpu.TsaParams.default()
+        ref = orc.score_batch(seqs, offs, orc.default_params(), nthreads=8)
+        ws = gpu.workspace_size(n, *ml, p, kernel)
+        d_ws = torch.empty(max(ws, 16), dtype=torch.uint8, device="cuda")
+        d_offs = torch.from_numpy(offs).cuda()
+        st = torch.cuda.current_stream().cuda_stream
+        out = []
+        for packed in (False, True):
+            d_seqs = torch.from_numpy(gpu.pack2(seqs) if packed else seqs).cuda()
+            d_sc = torch.zeros(n, dtype=torch.int32, device="cuda")
+            fn = gpu.score_batch_async_p2 if packed else gpu.score_batch_async
+            fn(d_seqs.data_ptr(), d_offs.data_ptr(), n, *ml, d_sc.data_ptr(), d_ws.data_ptr(), ws, st, p, kernel)
+            torch.cuda.synchronize()
+            out.append(d_sc.cpu().numpy())
+        assert np.array_equal(out[0], ref) and np.array_equal(out[1], ref), (kernel, n, L)

@@ -121,3 +121,17 @@ def test_testbench_initial_block_reader(tsa, orc, tmp_path):
         seqs = [tsa.read_sequence(tb, ram=f"seq{k}_ram", length=64) for k in "ABC"]
         assert all(len(x) == 64 and not x.any() for x in seqs)
         assert orc.score(*seqs) == 192
+
+
+def test_pack2_layout(tsa):
+    """tsa_pack2: four symbols per byte, symbol i at bits 2(i%4); N (4) packs
+    as A (the RTL's 2-bit symbol registers, src/PE_1cyc.v:63-66)."""
+    rng = np.random.default_rng(12)
+    for n in (0, 1, 3, 4, 5, 17, 64, 101):
+        s = rng.integers(0, 5, n).astype(np.uint8)
+        w = tsa.pack2(s)
+        assert len(w) == (n + 3) // 4
+        back = np.array([(int(w[i // 4]) >> (2 * (i % 4))) & 3 for i in range(n)], np.uint8)
+        assert np.array_equal(back, s & 3)
+    with pytest.raises(tsa.TsaError):
+        tsa.pack2(np.array([0, 5], np.uint8))
