@@ -57,6 +57,11 @@ int build_kparams(const tsa_params *p, KParams *kp) {
       {GO, GE, GO, GE, GO, GO, GE},            // Ixz :212-218
   };
   std::memcpy(kp->pen, t, sizeof(t));
+  for (int T = 0; T < 7; ++T)
+    for (int i = 0; i < 4; ++i) {
+      const int32_t lo = -t[T][2 * i], hi = -t[T][std::min(2 * i + 1, 6)];
+      kp->npen[T][i] = (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16);
+    }
   const int bits = p->score_bits;
   kp->bits = bits;
   kp->wrap_shift = bits ? 32 - bits : 0;

@@ -25,6 +25,7 @@ struct KParams {
   int32_t bits;           // SCORE_BITS wrap, 0 = none
   int32_t wrap_shift;     // 32 - bits, or 0 when bits == 0
   int32_t packed;         // input symbols 2-bit packed (tsa_score_batch_async_p2)
+  uint32_t npen[7][4];    // -P[T][s] as int16 pairs (s 0-1, 2-3, 4-5, 6-6): PLANE's packed form
 };
 
 // Symbol i of a sequence buffer: one byte per symbol, or 2-bit packed (four
@@ -47,15 +48,15 @@ Range value_bound(const tsa_params *p, int64_t la, int64_t lb, int64_t lc);
 // below a state (cdrop), for value_bound and the checked kernel.
 void bound_drops(const tsa_params *p, int64_t *drop, int64_t *cdrop);
 
-// Row stride (elements) of a (y,z) plane with lc+1 columns, padded so rows
-// start 16-byte aligned for int16 storage.
-inline int64_t plane_ldz(int64_t lc) { return ((lc + 1 + 7) / 8) * 8; }
+// Row stride (cells) of a (y,z) plane with lc+1 columns.
+inline int64_t plane_ldz(int64_t lc) { return lc + 1; }
 
 // ---- plane kernel (TSA_KERNEL_PLANE) --------------------------------------
+// A plane cell is the 7 int16 states + one pad: 16 bytes, one dwordx4.
 struct PlaneLayout {
-  int64_t ldz;          // row stride of a (y,z) plane
-  int64_t plane;        // elements per state-plane = (max_lb+1)*ldz
-  int64_t per_triple;   // elements per triple = 4 slots * 7 states * plane
+  int64_t ldz;          // row stride of a (y,z) plane, in cells
+  int64_t plane;        // cells per plane = (max_lb+1)*ldz
+  int64_t per_triple;   // cells per triple = 4 slots * plane
 };
 PlaneLayout plane_layout(int32_t max_lb, int32_t max_lc);
 size_t plane_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc);

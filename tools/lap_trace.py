@@ -6,7 +6,8 @@
 SPEC = LA[xLBxLC][:KEY=VAL,KEY=VAL...], e.g. 64, 256, 64x16x64:TSA_LAP_NW=8.
 Knobs are libtrialign environment knobs (TSA_PENCIL_MODE=lap is always set).
 Per spec one JSON line: the median event-timed latency of `reps` calls, then
-from one traced call the per-lap loop-begin lag (hand-off chain), each
+from one traced call the lap-to-lap lag of the loop ends (the hand-off
+chain), each
 workgroup's loop time per step (us and shader-clock cycles; the clock in MHz),
 loader stalls (tag re-fetches), wave 0's missed progress polls and
 the producers' back-pressure waits. Traces land in
@@ -113,11 +114,17 @@ def main():
                 if clk and dt > 0:
                     per_step_clk.append(clk / T)
                     mhz.append(clk / dt)
-            begins = [min(laps[k]) for k in sorted(laps)]
-            lags = [round(b1 - b0, 2) for b0, b1 in zip(begins, begins[1:])]
+            ends = {}
+            for r in rows:
+                lp = int(r["lap"])
+                ends[lp] = max(ends.get(lp, 0.0), us(r["loop_end"]))
+            # every workgroup starts at once (its prologue waits for nothing), so
+            # the chain shows in the loop ends: lap L+1 ends one hand-off after lap L
+            e = [ends[k] for k in sorted(ends)]
+            lags = [round(b1 - b0, 2) for b0, b1 in zip(e, e[1:])]
             rec.update({
                 "wgs": len(rows), "trace_total_us": round(max(us(r["loop_end"]) for r in rows), 2),
-                "lap_lag_us": {"median": round(statistics.median(lags), 2) if lags else None,
+                "lap_end_lag_us": {"median": round(statistics.median(lags), 2) if lags else None,
                                "max": max(lags) if lags else None, "first": lags[:4]},
                 "step_us": {"median": round(statistics.median(per_step_us), 4),
                             "max": round(max(per_step_us), 4)},
