@@ -14,7 +14,7 @@ OBJS     := $(patsubst $(PKG)/csrc/%.hip,$(PKG)/build/%.o,$(SRCS))
 
 ORACLE_SO  := oracle/_build/libtsa_oracle.so
 ORACLE_CLI := oracle/_build/tsa_oracle_cli
-ORACLE_SRC := oracle/tsa_oracle.c oracle/rtl_model.c
+ORACLE_SRC := oracle/tsa_oracle.c oracle/rtl_model.c oracle/rtl_model_2cyc.c
 
 all: $(LIB) $(CLI) oracle
 
@@ -32,11 +32,11 @@ $(CLI): $(PKG)/tools/tsa_cli.cpp $(LIB) include/trialign.h
 
 oracle: $(ORACLE_SO) $(ORACLE_CLI)
 
-$(ORACLE_SO): $(ORACLE_SRC) oracle/tsa_oracle.h include/trialign.h
+$(ORACLE_SO): $(ORACLE_SRC) oracle/tsa_oracle.h oracle/rtl_common.h include/trialign.h
 	@mkdir -p oracle/_build
 	gcc -O2 -std=c11 -Wall -fPIC -shared -o $@ $(ORACLE_SRC) -lpthread
 
-$(ORACLE_CLI): oracle/tsa_oracle_cli.c $(ORACLE_SRC) oracle/tsa_oracle.h
+$(ORACLE_CLI): oracle/tsa_oracle_cli.c $(ORACLE_SRC) oracle/tsa_oracle.h oracle/rtl_common.h
 	@mkdir -p oracle/_build
 	gcc -O2 -std=c11 -Wall -o $@ oracle/tsa_oracle_cli.c $(ORACLE_SRC) -lpthread
 

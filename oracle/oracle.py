@@ -60,6 +60,8 @@ def lib() -> ctypes.CDLL:
         L.tsao_rtl_run.argtypes = three + [ctypes.c_int32, i32p, i32p,
                                            ctypes.POINTER(ctypes.c_int64)]
         L.tsao_rtl_run.restype = ctypes.c_int
+        L.tsao_rtl2_run.argtypes = three + [i32p, i32p, ctypes.POINTER(ctypes.c_int64)]
+        L.tsao_rtl2_run.restype = ctypes.c_int
         L.tsao_align.argtypes = three + [pp, i32p, u8p, ctypes.c_int32, i32p, i32p]
         L.tsao_align.restype = ctypes.c_int
         L.tsao_gen_uniform.argtypes = [ctypes.c_uint64, u8p, ctypes.c_int32]
@@ -137,6 +139,19 @@ def rtl_run(a, b, c, a_total_len: int = 512) -> tuple[int, bool, int]:
                             ctypes.byref(isx), ctypes.byref(cyc))
     if rc:
         raise ValueError(f"rtl model rc={rc}")
+    return int(s.value), bool(isx.value), int(cyc.value)
+
+
+def rtl2_run(a, b, c) -> tuple[int, bool, int]:
+    """Cycle-level model of the 2-cycle RTL variant (oracle/rtl_model_2cyc.c):
+    (score, score_is_x, cycles)."""
+    A, B, C = _u8(a), _u8(b), _u8(c)
+    s, isx, cyc = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int64(0)
+    rc = lib().tsao_rtl2_run(_p(A, ctypes.c_uint8), len(A), _p(B, ctypes.c_uint8), len(B),
+                             _p(C, ctypes.c_uint8), len(C), ctypes.byref(s), ctypes.byref(isx),
+                             ctypes.byref(cyc))
+    if rc:
+        raise ValueError(f"rtl2 model rc={rc}")
     return int(s.value), bool(isx.value), int(cyc.value)
 
 

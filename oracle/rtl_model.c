@@ -29,28 +29,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "rtl_common.h"
 #include "tsa_oracle.h"
-
-#define XV INT32_MIN /* the X / z value */
-#define PE_LEN 8
-#define WS 12 /* SCORE_BITS = wordsize (src/TriAlign_tb.sv:56) */
-
-static inline int32_t w12(int64_t v) {
-  uint32_t u = (uint32_t)v << (32 - WS);
-  return (int32_t)u >> (32 - WS);
-}
-static inline int32_t addx(int32_t a, int32_t b) { return (a == XV || b == XV) ? XV : w12((int64_t)a + b); }
-static inline int32_t max2x(int32_t a, int32_t b) { return (a == XV || b == XV) ? XV : (a > b ? a : b); }
-/* MAX7 with the RTL's port grouping (src/PE_1cyc.v:22-28). */
-static inline int32_t max7x(int32_t g4, int32_t g2a, int32_t g2b, int32_t g3a, int32_t g1a,
-                            int32_t g1b, int32_t g3b) {
-  int32_t t1 = max2x(g1a, g1b), t2 = max2x(g2a, g2b), t3 = max2x(g3a, g3b);
-  return max2x(max2x(t1, t2), max2x(t3, g4));
-}
-
-typedef struct { int32_t s[7]; } st7; /* {M,Ix,Iy,Iz,Ixy,Iyz,Ixz} */
-static const st7 ZERO7 = {{0, 0, 0, 0, 0, 0, 0}};
-static const st7 X7 = {{XV, XV, XV, XV, XV, XV, XV}};
 
 typedef struct {
   int32_t A, B, C; /* 2-bit symbol regs, XV when z/x */
@@ -88,12 +68,6 @@ typedef struct {
 enum { IDLE = 0, INITIAL = 1, COMPUTE = 2 };
 #define SRAM_DEPTH 512 /* 2**SRAM_ADDR_BITS, SRAM_ADDR_BITS = 9 */
 #define AMASK 511u
-
-static int32_t tb_symbol(const uint8_t *s, int len, uint32_t addr) {
-  /* caller RAM: defined only where the caller wrote a symbol */
-  if ((int64_t)addr >= len) return XV;
-  return (int32_t)(s[addr] & 0xF);
-}
 
 /* PE wire outputs (M_o is z when EN==0, src/PE_1cyc.v:148) */
 static inline st7 pe_out(const pe_t *p) {
@@ -190,69 +164,10 @@ int tsao_rtl_run(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
         pe_t *n = &npe[ge][gi];
         const int EN_i = ENo[ge - 1][gi];
         const st7 i1 = Mo[ge - 1][gi - 1], i2 = Mo[ge - 1][gi], i3 = Mo[ge][gi - 1];
-        const int32_t MATCH = 1, MISMATCH = -1, GO = 2, GE = 1;
-        const int32_t GO2 = GO << 1, GE2 = GE << 1, GOGE = GO + GE;
-        int32_t tAB, tBC, tAC, tABC;
-        if (p->A == XV || p->B == XV) tAB = XV; else tAB = (p->A == p->B) ? MATCH : MISMATCH;
-        if (p->B == XV || p->C == XV) tBC = XV; else tBC = (p->B == p->C) ? MATCH : MISMATCH;
-        if (p->A == XV || p->C == XV) tAC = XV; else tAC = (p->A == p->C) ? MATCH : MISMATCH;
-        if (p->A == XV || p->B == XV || p->C == XV) tABC = XV;
-        else if (p->A == p->B) tABC = (p->B == p->C) ? ((p->A == p->C) ? MATCH * 3 : (MATCH << (1 + MISMATCH))) : w12((int64_t)(MATCH + MISMATCH) * 2);
-        else tABC = w12(MISMATCH * 3);
-        const int gate = (EN_i == 1 && p->EN == 0);
-        const st7 *d2 = &p->d2_1, *own = &p->S, *d21 = &p->d1_2, *d31 = &p->d1_3, *d11 = &p->d1_1;
-#define C0(pen, sc) addx(-(pen), (sc))
-#define CV(v, pen, sc) addx(addx((v), -(pen)), (sc))
-        /* M (164-170) */
-        int32_t mM = gate ? C0(0, tABC) : CV(d2->s[0], 0, tABC);
-        int32_t mIx = gate ? C0(0, tABC) : CV(d2->s[1], 0, tABC);
-        int32_t mIy = gate ? C0(0, tABC) : CV(d2->s[2], 0, tABC);
-        int32_t mIz = gate ? C0(0, tABC) : CV(d2->s[3], 0, tABC);
-        int32_t mIxy = gate ? C0(0, tABC) : CV(d2->s[4], 0, tABC);
-        int32_t mIyz = gate ? C0(0, tABC) : CV(d2->s[5], 0, tABC);
-        int32_t mIxz = gate ? C0(0, tABC) : CV(d2->s[6], 0, tABC);
-        n->S.s[0] = max7x(mM, mIxy, mIyz, mIz, mIx, mIy, mIxz);
-        /* Ix (172-178) */
-        int32_t xM = gate ? -GO2 : CV(own->s[0], GO2, 0);
-        int32_t xIx = gate ? -GE2 : CV(own->s[1], GE2, 0);
-        int32_t xIy = gate ? -GOGE : CV(own->s[2], GOGE, 0);
-        int32_t xIz = gate ? -GOGE : CV(own->s[3], GOGE, 0);
-        int32_t xIxy = gate ? -GOGE : CV(own->s[4], GOGE, 0);
-        int32_t xIyz = gate ? -GO2 : CV(own->s[5], GO2, 0);
-        int32_t xIxz = gate ? -GOGE : CV(own->s[6], GOGE, 0);
-        n->S.s[1] = max7x(xIx, xIxy, xIxz, xIy, xM, xIyz, xIz);
-        /* Iy (180-186) */
-        n->S.s[2] = max7x(CV(i2.s[2], GE2, 0), CV(i2.s[4], GOGE, 0), CV(i2.s[5], GOGE, 0),
-                          CV(i2.s[1], GOGE, 0), CV(i2.s[0], GO2, 0), CV(i2.s[6], GO2, 0),
-                          CV(i2.s[3], GOGE, 0));
-        /* Iz (188-194) */
-        n->S.s[3] = max7x(CV(i3.s[3], GE2, 0), CV(i3.s[6], GOGE, 0), CV(i3.s[5], GOGE, 0),
-                          CV(i3.s[1], GOGE, 0), CV(i3.s[0], GO2, 0), CV(i3.s[4], GO2, 0),
-                          CV(i3.s[2], GOGE, 0));
-        /* Ixy (196-202) */
-        int32_t aM = gate ? C0(GO, tAB) : CV(d21->s[0], GO, tAB);
-        int32_t aIx = gate ? C0(GE, tAB) : CV(d21->s[1], GE, tAB);
-        int32_t aIy = gate ? C0(GE, tAB) : CV(d21->s[2], GE, tAB);
-        int32_t aIz = gate ? C0(GO, tAB) : CV(d21->s[3], GO, tAB);
-        int32_t aIxy = gate ? C0(GE, tAB) : CV(d21->s[4], GE, tAB);
-        int32_t aIyz = gate ? C0(GO, tAB) : CV(d21->s[5], GO, tAB);
-        int32_t aIxz = gate ? C0(GO, tAB) : CV(d21->s[6], GO, tAB);
-        n->S.s[4] = max7x(aIy, aIxy, aIx, aIyz, aM, aIxz, aIz);
-        /* Iyz (204-210) */
-        n->S.s[5] = max7x(CV(d11->s[3], GE, tBC), CV(d11->s[6], GO, tBC), CV(d11->s[1], GO, tBC),
-                          CV(d11->s[5], GE, tBC), CV(d11->s[0], GO, tBC), CV(d11->s[4], GO, tBC),
-                          CV(d11->s[2], GE, tBC));
-        /* Ixz (212-218) */
-        int32_t cM = gate ? C0(GO, tAC) : CV(d31->s[0], GO, tAC);
-        int32_t cIx = gate ? C0(GE, tAC) : CV(d31->s[1], GE, tAC);
-        int32_t cIy = gate ? C0(GO, tAC) : CV(d31->s[2], GO, tAC);
-        int32_t cIz = gate ? C0(GE, tAC) : CV(d31->s[3], GE, tAC);
-        int32_t cIxy = gate ? C0(GO, tAC) : CV(d31->s[4], GO, tAC);
-        int32_t cIyz = gate ? C0(GO, tAC) : CV(d31->s[5], GO, tAC);
-        int32_t cIxz = gate ? C0(GE, tAC) : CV(d31->s[6], GE, tAC);
-        n->S.s[6] = max7x(cIz, cIxy, cIyz, cIxz, cM, cIx, cIy);
-#undef C0
-#undef CV
+        int32_t cand[7][7];
+        pe_cands(p->A, p->B, p->C, EN_i == 1 && p->EN == 0, &p->S, &p->d2_1, &p->d1_1, &p->d1_2,
+                 &p->d1_3, &i2, &i3, cand);
+        n->S = pe_max(cand);
         /* delay + input registers (247-299) */
         n->d2_1 = p->d1_1;
         n->d1_1 = i1;

@@ -93,6 +93,12 @@ int tsao_rtl_run(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
                  const uint8_t *c, int32_t lc, int32_t a_total_len, int32_t *score,
                  int32_t *score_is_x, int64_t *cycles_out);
 
+/* Cycle-level model of TRIALIGN_2cyc + PE_2cyc (oracle/rtl_model_2cyc.c),
+ * A_TOTAL_LEN 512 (la <= 512). Same outputs as tsao_rtl_run. */
+int tsao_rtl2_run(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
+                  const uint8_t *c, int32_t lc, int32_t *score, int32_t *score_is_x,
+                  int64_t *cycles_out);
+
 /* Monotonic wall clock in seconds (clock_gettime(CLOCK_MONOTONIC)). */
 double tsao_now(void);
 

@@ -3,7 +3,11 @@
 Fixtures are data only: inputs + expected outputs. Expected values come from
 the CPU restatement (oracle/tsa_oracle.c, literal RTL arithmetic) and, for
 inputs inside the RTL envelope, from the cycle-level RTL model
-(oracle/rtl_model.c); the script asserts the two agree before writing.
+(oracle/rtl_model.c); the script asserts the two agree before writing. Every
+default-parameter case with lengths that are multiples of 8 (LA <= 512) also
+records the 2-cycle RTL model's result (oracle/rtl_model_2cyc.c) and whether
+it agrees -- the 2-cycle variant's y-face SRAM banking breaks some shapes,
+non-power-of-two cubes among them.
 Inputs: the reference's own dat triple (dat/{A,B,C}_seq.dat, copied as
 numbers), the testbench's all-A input (src/TriAlign_tb.sv:423-1960), prefixes,
 homopolymers, seeded random triples (uniform + related), RTL and SOP scoring,
@@ -45,6 +49,9 @@ def case(name, a, b, c, **pk):
         r, isx, cyc = oracle.rtl_run(a, b, c)
         assert not isx and r == s, (name, r, isx, s)
         rec["rtl_model"] = {"score": r, "cycles": cyc}
+    if default and all(n % 8 == 0 for n in (len(a), len(b), len(c))) and len(a) <= 512:
+        r2, isx2, cyc2 = oracle.rtl2_run(a, b, c)
+        rec["rtl2_model"] = {"score": r2, "x": isx2, "cycles": cyc2, "agrees": (not isx2) and r2 == s}
     return rec
 
 
@@ -82,7 +89,15 @@ def main():
     cases.append(case("wrap6_rand", rng.integers(0, 4, 30), rng.integers(0, 4, 30), rng.integers(0, 4, 30), score_bits=6))
     cases.append(case("bits16_params", rng.integers(0, 4, 20), rng.integers(0, 4, 25), rng.integers(0, 4, 18),
                       match=5, mismatch=-4, gap_open=10, gap_extend=1, score_bits=16))
-    out = {"generator": "tests/golden/make_golden.py", "oracle": "oracle/tsa_oracle.c (+ rtl_model.c)",
+    # cubes and near-cubes for the 2-cycle variant: power-of-two and other
+    # sizes, LB != LA, a single z pencil (no y face ever read)
+    r3 = np.random.default_rng(2026)
+    for la, lb, lc in ((8, 8, 8), (16, 16, 16), (24, 24, 24), (32, 32, 32), (40, 40, 40),
+                       (48, 48, 48), (56, 56, 56), (64, 64, 64), (72, 72, 72), (80, 80, 80),
+                       (96, 96, 96), (64, 64, 32), (64, 32, 64), (32, 64, 8), (48, 48, 96)):
+        a, b, c = (r3.integers(0, 4, n).astype(np.uint8) for n in (la, lb, lc))
+        cases.append(case(f"cube2_{la}x{lb}x{lc}", a, b, c))
+    out = {"generator": "tests/golden/make_golden.py", "oracle": "oracle/tsa_oracle.c (+ rtl_model.c, rtl_model_2cyc.c)",
            "cases": cases}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.json")
     with open(path, "w") as f:

@@ -53,6 +53,65 @@ def test_rtl_model_long_pencil_ring(orc):
     assert cyc == (64 // 8) * (40 // 8) * (65 + 128 + 16) + 1
 
 
+def test_rtl2_model_testbench_and_dat(orc, golden):
+    """The 2-cycle variant (oracle/rtl_model_2cyc.c) on the testbench's own
+    input and the reference's dat triple: the same scores as the 1-cycle
+    variant and the restatement."""
+    z = [0] * 64
+    r, isx, cyc = orc.rtl2_run(z, z, z)
+    assert (r, isx) == (192, False)
+    # per pencil 65 INITIAL clocks, then a COMPUTE + WAIT pair per step for
+    # A_idx + 16 steps (src/TriAlign_2cyc.v:354-355,433-482)
+    assert cyc == 64 * (65 + 2 * (64 + 16)) + 1
+    by = {c["name"]: c for c in golden}
+    assert by["dat"]["rtl2_model"] == {"score": 1, "x": False, "cycles": cyc, "agrees": True}
+
+
+def test_golden_rtl2_records(orc, golden, tsa):
+    """golden.json records, for every default-parameter case the 2-cycle RTL
+    can take, its model's score and whether it agrees with the restatement;
+    agreement is exactly the 2-cycle envelope (rtl_envelope(variant="2cyc"))."""
+    seen = 0
+    for c in golden:
+        r = c.get("rtl2_model")
+        if r is None:
+            continue
+        seen += 1
+        la, lb, lc = len(c["a"]), len(c["b"]), len(c["c"])
+        assert r["agrees"] == ((not r["x"]) and r["score"] == c["score"]), c["name"]
+        assert r["agrees"] == tsa.rtl_envelope(la, lb, lc, variant="2cyc"), c["name"]
+        if la * lb * lc <= 64 ** 3:
+            s, isx, cyc = orc.rtl2_run(c["a"], c["b"], c["c"])
+            assert (s, isx, cyc) == (r["score"], r["x"], r["cycles"]), c["name"]
+    assert seen >= 30
+
+
+RTL2_SHAPES = [(n, n, n) for n in range(8, 137, 8)] + [
+    (64, 32, 64), (64, 64, 32), (64, 64, 8), (32, 64, 8), (128, 64, 64), (64, 64, 128),
+    (48, 48, 96), (96, 96, 16), (40, 40, 80)]
+
+
+def test_rtl2_envelope_is_where_the_model_agrees(orc, tsa):
+    """The 2-cycle variant's y-face store (3 groups x 2 x 8 SRAMs, group and
+    page from index bits shared with B_idx, src/TriAlign_2cyc.v:85-92,141-157,
+    176-180) only carries every face to its reader for some shapes: LB = LA
+    (or a single z pencil), and no bank shared by a pencil's write, read and
+    corner slots -- 8, 16, 40, 48, 64, 128 cubes here; 24, 32, 56, 72-120,
+    136 cubes and LB != LA come back X or wrong. The host-side rule
+    (_rtl2_ring_ok) is checked against the clocked model on every shape."""
+    for la, lb, lc in RTL2_SHAPES:
+        agree = []
+        for seed in range(3):
+            rng = np.random.default_rng(seed)
+            a, b, c = (rng.integers(0, 4, n).astype(np.uint8) for n in (la, lb, lc))
+            s, isx, _ = orc.rtl2_run(a, b, c)
+            agree.append((not isx) and s == orc.score(a, b, c))
+        want = tsa.rtl_envelope(la, lb, lc, variant="2cyc")
+        assert (all(agree) if want else not all(agree)), ((la, lb, lc), agree, want)
+    assert tsa.rtl_envelope(64, 64, 64, variant="2cyc") and tsa.rtl_envelope(256, 256, 256, variant="2cyc")
+    assert not tsa.rtl_envelope(96, 96, 96, variant="2cyc") and tsa.rtl_envelope(96, 96, 96)
+
+
 def test_factored_form_equals_literal(orc):
     rng = np.random.default_rng(11)
     for k in range(40):
