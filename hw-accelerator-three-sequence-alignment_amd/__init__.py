@@ -63,6 +63,7 @@ EXPORTS = (
     "tsa_score_batch", "tsa_batch_workspace_size", "tsa_score_batch_async",
     "tsa_device_count", "tsa_strerror", "tsa_version", "tsa_describe_plan", "tsa_align_gpu",
     "tsa_fallback_count", "tsa_check_fallback_count", "tsa_score_batch_async_p2", "tsa_pack2",
+    "tsa_score_gpu_multi",
 )
 
 # Score of a triple the device could not score (include/trialign.h).
@@ -136,6 +137,9 @@ def _load_lib() -> ctypes.CDLL:
                                                             ctypes.c_char_p, ctypes.c_size_t]
     lib.tsa_align_gpu.argtypes = [u8p, ctypes.c_int32, u8p, ctypes.c_int32, u8p, ctypes.c_int32,
                                   pp, i32p, u8p, ctypes.c_int32, i32p, i32p, ctypes.c_int32]
+    lib.tsa_score_gpu_multi.argtypes = [u8p, ctypes.c_int32, u8p, ctypes.c_int32, u8p,
+                                        ctypes.c_int32, pp, i32p, ctypes.c_int32, i32p,
+                                        ctypes.POINTER(ctypes.c_double)]
     lib.tsa_fallback_count.argtypes = []
     lib.tsa_fallback_count.restype = ctypes.c_int64
     lib.tsa_score_batch_async_p2.argtypes = lib.tsa_score_batch_async.argtypes
@@ -149,7 +153,8 @@ def _load_lib() -> ctypes.CDLL:
     lib.tsa_version.restype = ctypes.c_char_p
     for name in ("tsa_validate", "tsa_score_gpu", "tsa_score_gpu_ex", "tsa_score_batch",
                  "tsa_batch_workspace_size", "tsa_score_batch_async", "tsa_device_count",
-                 "tsa_describe_plan", "tsa_align_gpu", "tsa_score_batch_async_p2", "tsa_pack2"):
+                 "tsa_describe_plan", "tsa_align_gpu", "tsa_score_batch_async_p2", "tsa_pack2",
+                 "tsa_score_gpu_multi"):
         getattr(lib, name).restype = ctypes.c_int
     return lib
 
@@ -229,6 +234,24 @@ def score(a, b, c, params: Optional[TsaParams] = None, kernel: str | int = "auto
     if final_states:
         return int(out.value), tuple(int(v) for v in fin)
     return int(out.value)
+
+
+def score_multi(a, b, c, devices: Sequence[int], params: Optional[TsaParams] = None):
+    """One triple's cube split over several GPUs by laps (tsa_score_gpu_multi):
+    ``(score, wall_us)``. The reference's pencil slicing with face SRAMs
+    between pencils (src/TriAlign_1cyc.v:78-98,127-140) spread over devices;
+    a device listed twice runs two concurrent parts on one GPU."""
+    p = params or TsaParams.default()
+    A, B, C = _as_u8(a), _as_u8(b), _as_u8(c)
+    devs = np.ascontiguousarray(np.asarray(list(devices), dtype=np.int32))
+    out = ctypes.c_int32(0)
+    wall = ctypes.c_double(0.0)
+    rc = _lib.tsa_score_gpu_multi(_ptr(A, ctypes.c_uint8), len(A), _ptr(B, ctypes.c_uint8), len(B),
+                                  _ptr(C, ctypes.c_uint8), len(C), ctypes.byref(p),
+                                  _ptr(devs, ctypes.c_int32), len(devs), ctypes.byref(out),
+                                  ctypes.byref(wall))
+    _check(rc, "tsa_score_gpu_multi")
+    return int(out.value), float(wall.value)
 
 
 def align(a, b, c, params: Optional[TsaParams] = None, device: int = 0):

@@ -31,6 +31,8 @@ constexpr int64_t LAP_MAX_WAVES = 3;
 LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW,
                  bool full_rings, bool f16, bool sop);
 size_t lap_workspace_bytes(const LapGeom &g);
+// The launch's error word inside a workspace of n triples (set on a hand-off timeout).
+uint32_t *lap_err_word(const LapGeom &g, int32_t n, void *d_ws);
 // Launch it. d_err (synchronous callers): the error word, cleared before the
 // launch, nonzero after it when a hand-off timed out.
 // chk (int16 form only): the checked kernel, then a certification pass that
@@ -39,5 +41,28 @@ int lap_launch(const LapGeom &g, bool f16, bool sop, const uint8_t *d_seqs,
                const int64_t *d_offsets, int32_t n, int32_t *d_scores, void *d_ws,
                const PencilArgs &pa, hipStream_t stream, int32_t **d_err,
                const CheckLimits *chk = nullptr);
+
+// One part of a single cube split over devices by laps (tsa_score_gpu_multi):
+// laps [L0, L1) on `device`, with that device's copy of the triple and a
+// fine-grained workspace of lap_workspace_bytes(g) (peers write into it).
+struct LapPart {
+  int device;
+  hipStream_t stream;
+  int32_t L0, L1;
+  const uint8_t *d_seqs;
+  const int64_t *d_offsets;
+  void *d_ws;
+};
+// Launch every part (parts in lap order, covering [0, g.G)); d_score and the
+// error word d_err (cleared by the caller) are on the last part's device.
+int lap_launch_split(const LapGeom &g, bool f16, bool sop, const PencilArgs &pa, const LapPart *parts,
+                     int np, int32_t *d_score, uint32_t *d_err);
+// The lap geometry of one (la, lb, lc) cube for an np-way split (.ok = false
+// when the factored form has no lap schedule for it or fewer than np laps),
+// and its launch (arithmetic chosen as pencil_launch_batch would).
+LapGeom pencil_split_geom(int32_t la, int32_t lb, int32_t lc, const KParams &kp, const Range &bound,
+                          int np);
+int pencil_launch_split(const LapGeom &g, const KParams &kp, const Range &bound, const LapPart *parts,
+                        int np, int32_t *d_score, uint32_t *d_err);
 
 }  // namespace tsa

@@ -109,9 +109,15 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // The s_nop: a VMEM store of more than 8 bytes must not have its data VGPRs
 // rewritten by the next VALU instruction (one wait state); the compiler's
 // hazard recognizer does not look inside inline asm, so the asm carries it.
+// SYS (a cube split over devices, lap_launch_split): system scope (sc0 sc1),
+// so a record written into a peer device's fine-grained ring is visible there.
+template <bool SYS = false>
 __device__ __forceinline__ void store16_sc1(void *gptr, uint4 v) {
   const u32x4 d = {v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(gptr), "v"(d) : "memory");
+  if constexpr (SYS)
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(gptr), "v"(d) : "memory");
+  else
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(gptr), "v"(d) : "memory");
 }
 __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
   return __builtin_amdgcn_perm(s0, s1, sel);
@@ -314,16 +320,25 @@ __device__ __forceinline__ void static_for(F &&f) {
 // folded into a per-lane max / min; each wave's extremes go to mon[tri]
 // (max) and mon[n + tri] (min) by atomics, and lap_certify() decides whether
 // any candidate of the literal RTL recurrence could have wrapped.
-template <int M, int NW, bool F16, bool SOP, bool CHK>
+// A launch runs laps [L0, L1) of the cube (a single launch: [0, G)). SYS: one
+// part of a cube split over devices (lap_launch_split) -- every hand-off load
+// and store at system scope, the y ring of lap L1-1 written into the next
+// part's workspace (yf_out, its consumer's memory) and the progress words of
+// lap L0 into the previous part's (prog_in, its producer's memory), so every
+// poll reads local memory and only posted stores cross the link.
+template <int M, int NW, bool F16, bool SOP, bool CHK, bool SYS = false>
 __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel(
     const uint8_t *__restrict__ seqs, const int64_t *__restrict__ offs, int32_t G, int32_t GZ,
     int32_t NC, int32_t CH, int32_t YR, int32_t ZR, uint8_t *__restrict__ yf_base,
     uint8_t *__restrict__ zf_base, int32_t *__restrict__ prog, uint32_t *__restrict__ err,
     int32_t *__restrict__ scores, int32_t *__restrict__ mon, PencilArgs pa, uint32_t epoch,
-    uint32_t spin_limit,
+    uint32_t spin_limit, int32_t L0, int32_t L1, uint8_t *__restrict__ yf_out,
+    int32_t *__restrict__ prog_in,
     unsigned long long *__restrict__ trace) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   static_assert(!(CHK && F16), "the checked kernel runs the int16 form");
+  static_assert(!(CHK && SYS), "a split cube runs the unchecked forms");
+  constexpr int SCOPE = SYS ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
   constexpr int RW = 2 * NW, ZT = 64 * M, LPD = lap_pd(M), K = lap_k(M), K0 = lap_k0(M);
   constexpr int PAIR = 64 * REC_BYTES, SLOT = M * PAIR;
   // wave w's rows sit at step offsets 2w (low half) and 2w + 1 (high); lap L+1
@@ -348,8 +363,8 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
   // b = 8 * (L*CH + c/8) + c%8 -- a column's laps share b % 8 (one XCD), and
   // every producer ((L-1, c), (L, c-1)) has a lower block index than its consumer
   const int32_t b = blockIdx.x, slot = b >> 3;
-  const int32_t L = slot / CH, col = (slot % CH) * 8 + (b & 7);
-  if (col >= NC) return;  // padding block
+  const int32_t L = L0 + slot / CH, col = (slot % CH) * 8 + (b & 7);
+  if (col >= NC || L >= L1) return;  // padding block
   const int32_t tri = col / GZ, q = col % GZ;
   const int64_t o0 = offs[3 * (int64_t)tri], o1 = offs[3 * (int64_t)tri + 1];
   const int64_t o2 = offs[3 * (int64_t)tri + 2], o3 = offs[3 * (int64_t)tri + 3];
@@ -379,7 +394,10 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
   const int32_t T = final_wg ? (la - 1) + tau(r_f) + k_f + 1 : la + tau(rows - 1) + zt_q - 1;
   const int32_t T_above = la + tau(RW - 1) + zt_q - 1;  // records the lap above writes (same tile)
   const int32_t T_left = la + tau(rows - 1) + ZT - 1;   // z records the tile to the left writes
-  uint8_t *yf_mine = yf_base + lid * YR * SLOT;
+  uint8_t *yf_mine = (L == L1 - 1 ? yf_out : yf_base) + lid * YR * SLOT;  // in my consumer's memory
+  // my progress word: read by the z producer (same part, local) and the y
+  // producer -- at lap L0 of a split cube the previous part, so a copy goes there
+  int32_t *const prog_x = (SYS && L == L0 && L0 > 0) ? prog_in + lid * LAP_PROG_STRIDE : nullptr;
   const uint8_t *yf_prev = yin ? yf_base + (lid - GZ) * YR * SLOT : yf_mine;
   uint8_t *zf_mine = zf_base + lid * ZR * ZREC;
   const uint8_t *zf_prev = zin ? zf_base + (lid - 1) * ZR * ZREC : zf_mine;
@@ -387,7 +405,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
   bool timed_out = false;
   auto fail = [&]() {  // every wait of this workgroup gives up from now on
     if (!timed_out && lane == 0) {
-      __hip_atomic_store(err, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(err, epoch, __ATOMIC_RELEASE, SCOPE);
       *(volatile __attribute__((address_space(3))) int32_t *)(__attribute__((address_space(3))) void *)w_abort = 1;
     }
     timed_out = true;
@@ -445,8 +463,8 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
     // written to LDS (xr0 / zring) and published.
     uint32_t stalls = 0;
     typedef unsigned long long u64;
-    auto gl8 = [](const uint8_t *p) -> u64 {
-      return __hip_atomic_load((const u64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    auto gl8 = [&](const uint8_t *p) -> u64 {
+      return __hip_atomic_load((const u64 *)p, __ATOMIC_RELAXED, SCOPE);
     };
     const int64_t cons_y = yout ? lid + GZ : lid, cons_z = zout ? lid + 1 : lid;
     struct Fetch {
@@ -470,8 +488,8 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
     auto fetch = [&](int32_t s, Fetch &f) {
       fetch_y(s, f);
       fetch_z(s + ZT + ZA, f);
-      f.py = __hip_atomic_load(prog + cons_y * LAP_PROG_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      f.pz = __hip_atomic_load(prog + cons_z * LAP_PROG_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      f.py = __hip_atomic_load(prog + cons_y * LAP_PROG_STRIDE, __ATOMIC_RELAXED, SCOPE);
+      f.pz = __hip_atomic_load(prog + cons_z * LAP_PROG_STRIDE, __ATOMIC_RELAXED, SCOPE);
     };
     auto tag_ok = [](u64 g, uint32_t tg) { return (uint32_t)(g >> 32) == tg; };
     auto y_ok = [&](int32_t s, const Fetch &f) {
@@ -662,7 +680,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       ++n_bp;
       for (uint32_t spin = 0;; ++spin) {
         const int32_t v = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(prog + cons * LAP_PROG_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            __hip_atomic_load(prog + cons * LAP_PROG_STRIDE, __ATOMIC_RELAXED, SCOPE));
         seen = max(seen, prog_decode(v));
         if (need <= seen) return;
         if (spin >= spin_limit || timed_out || ((spin & 63) == 63 && lds_word(w_abort) != 0)) {
@@ -837,16 +855,20 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
           const uint32_t tg = lap_tag(epoch, t);
 #pragma unroll
           for (int i = 0; i < M; ++i)
-            store16_sc1(yf_mine + ((int64_t)(t & (YR - 1)) * M + i) * PAIR + lane * REC_BYTES,
+            store16_sc1<SYS>(yf_mine + ((int64_t)(t & (YR - 1)) * M + i) * PAIR + lane * REC_BYTES,
                         make_uint4(perm(oIxy[i], oIy[i], 0x07060302u), tg,
                                    perm(oBest[i], oIyz[i], 0x07060302u), tg));
         }
         // my producers' back-pressure: the loader has checked at least
         // t - NW + 2 steps (wave 0 ran t - NW + 1 before this wave's step t)
         if ((yin || zin) && (t & (LAP_PUB - 1)) == 0 && lane == 0)
-          __hip_atomic_store(prog + lid * LAP_PROG_STRIDE,
-                             (int32_t)((ep19 << 13) | (uint32_t)max(t - NW + 2, 0)),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        {
+          const int32_t pv_ = (int32_t)((ep19 << 13) | (uint32_t)max(t - NW + 2, 0));
+          __hip_atomic_store(prog + lid * LAP_PROG_STRIDE, pv_, __ATOMIC_RELAXED, SCOPE);
+          if constexpr (SYS) {
+            if (prog_x != nullptr) __hip_atomic_store(prog_x, pv_, __ATOMIC_RELAXED, SCOPE);
+          }
+        }
       }
       // ---- z record of this wave's last position (lane 63, register M-1)
       if (zout) {
@@ -854,8 +876,8 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
         if (lane == 63) {
           const uint32_t tg = lap_tag(epoch, t);
           uint8_t *zdst = zf_mine + (int64_t)(t & (ZR - 1)) * ZREC + w * LAP_ZREC_WAVE;
-          store16_sc1(zdst, make_uint4(oIz[M - 1], tg, oIxz[M - 1], tg));
-          store16_sc1(zdst + 16, make_uint4(Ryz[M - 1], tg, Rb[M - 1], tg));
+          store16_sc1<SYS>(zdst, make_uint4(oIz[M - 1], tg, oIxz[M - 1], tg));
+          store16_sc1<SYS>(zdst + 16, make_uint4(Ryz[M - 1], tg, Rb[M - 1], tg));
         }
       }
       lds_publish(pw + 64 * w, t + 1, lane);
@@ -955,7 +977,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
     const uint16_t hb = (uint16_t)(hf ? (v >> 16) : (v & 0xFFFF));
     // a timed-out hand-off anywhere upstream invalidates the score (every
     // workgroup of the triple precedes this one): report it in-band
-    const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+    const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, SCOPE) == epoch;
     scores[tri] = bad ? TSA_SCORE_INVALID
                       : F16 ? (int32_t)(float)__builtin_bit_cast(_Float16, hb) : (int32_t)(int16_t)hb;
   }
@@ -1075,6 +1097,9 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
 }
 
 size_t lap_workspace_bytes(const LapGeom &g) { return g.prog_bytes + g.yf_bytes + g.zf_bytes; }
+uint32_t *lap_err_word(const LapGeom &g, int32_t n, void *d_ws) {
+  return (uint32_t *)((int32_t *)d_ws + (int64_t)n * g.G * g.GZ * LAP_PROG_STRIDE);
+}
 
 static uint32_t lap_spin_limit() {
   if (const char *e = getenv("TSA_LAP_SPIN_LIMIT")) return (uint32_t)strtoul(e, nullptr, 0);
@@ -1115,7 +1140,7 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
   const uint32_t epoch = lap_next_epoch();
   hipLaunchKernelGGL(kfn, dim3((uint32_t)g.blocks), dim3(64 * (NW + 1)), g.lds, stream, d_seqs,
                      d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, prog, err, d_scores, mon, pa,
-                     epoch, lap_spin_limit(), trace);
+                     epoch, lap_spin_limit(), 0, g.G, yf, prog, trace);
   if (chk) {
     if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
     hipLaunchKernelGGL(lap_certify, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, mon, n,
@@ -1159,6 +1184,48 @@ int lap_launch(const LapGeom &g, bool f16, bool sop, const uint8_t *d_seqs,
   }
   return TSA_LAP_SHAPES(launch_lap, g.M, g.NW, f16, sop, d_seqs, d_offsets, n, g, d_scores, d_ws,
                         pa, stream, chk);
+}
+
+// ---------------------------------------------------------------------------
+// One cube split over devices by laps (tsa_score_gpu_multi): part p runs laps
+// [L0_p, L1_p) on its own device; part p's last lap writes its y records into
+// part p+1's workspace and part p+1's first lap copies its progress words into
+// part p's, so each hand-off crossing the link is a posted store and every
+// poll stays local. The error word and the score live with the last part.
+template <int M, int NW, bool F16, bool SOP>
+static int launch_lap_split(const LapGeom &g, const PencilArgs &pa, const LapPart *parts, int np,
+                            int32_t *d_score, uint32_t *d_err) {
+  auto kfn = lap_kernel<M, NW, F16, SOP, false, true>;
+  const uint32_t epoch = lap_next_epoch();
+  const uint32_t spin = lap_spin_limit();
+  for (int p = 0; p < np; ++p) {
+    const LapPart &q = parts[p];
+    if (hipSetDevice(q.device) != hipSuccess) return TSA_EDEVICE;
+    if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)g.lds) != hipSuccess)
+      return TSA_EDEVICE;
+    int32_t *prog = (int32_t *)q.d_ws;
+    uint8_t *yf = (uint8_t *)q.d_ws + g.prog_bytes;
+    uint8_t *zf = yf + g.yf_bytes;
+    uint8_t *yf_out = p + 1 < np ? (uint8_t *)parts[p + 1].d_ws + g.prog_bytes : yf;
+    int32_t *prog_in = p > 0 ? (int32_t *)parts[p - 1].d_ws : prog;
+    const int64_t blocks = (int64_t)(q.L1 - q.L0) * g.CH * 8;
+    hipLaunchKernelGGL(kfn, dim3((uint32_t)blocks), dim3(64 * (NW + 1)), g.lds, q.stream, q.d_seqs,
+                       q.d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, prog, d_err, d_score,
+                       (int32_t *)nullptr, pa, epoch, spin, q.L0, q.L1, yf_out, prog_in,
+                       (unsigned long long *)nullptr);
+    if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
+  }
+  return TSA_OK;
+}
+
+int lap_launch_split(const LapGeom &g, bool f16, bool sop, const PencilArgs &pa, const LapPart *parts,
+                     int np, int32_t *d_score, uint32_t *d_err) {
+  if (np < 1 || g.lds > LDS_MAX) return TSA_EINVAL;
+  for (int p = 0; p < np; ++p)
+    if (parts[p].L0 >= parts[p].L1 || parts[p].L0 != (p ? parts[p - 1].L1 : 0)) return TSA_EINVAL;
+  if (parts[np - 1].L1 != g.G) return TSA_EINVAL;
+  return TSA_LAP_SHAPES(launch_lap_split, g.M, g.NW, f16, sop, g, pa, parts, np, d_score, d_err);
 }
 
 }  // namespace tsa

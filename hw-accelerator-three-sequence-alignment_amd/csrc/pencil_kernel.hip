@@ -750,6 +750,33 @@ int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t
   return TSA_SHAPES(launch_m, g.M, helix_nw(g.M), f16, sop, d_seqs, d_offsets, n, max_lb, g,
                     d_scores, d_ws, pa, stream);
 }
+
+// A single cube split over np devices by laps: the lap schedule of this cube
+// (whatever the helix would cost), if it has at least np laps.
+LapGeom pencil_split_geom(int32_t la, int32_t lb, int32_t lc, const KParams &kp, const Range &bound,
+                          int np) {
+  LapGeom g{};
+  g.ok = false;
+  if (np < 1 || !pencil_shape_ok(la, lb, lc)) return g;
+  const bool f16 = use_f16(kp, bound), sop = kp.s3_mode == TSA_S3_SOP;
+  g = lap_choice(1, la, lb, lc, LAP_RESIDENT, f16, sop, true);
+  if (!g.ok || g.G < np) {
+    g.ok = false;
+    return g;
+  }
+  // full-length rings: no producer ever waits for its consumer, so a part
+  // whose launch queues behind an earlier part (parts sharing a hardware
+  // queue) cannot deadlock it -- the only waits point from later parts to
+  // earlier ones, which are launched first
+  return lap_geom(1, la, lb, lc, g.M, g.NW, true, f16, sop);
+}
+
+int pencil_launch_split(const LapGeom &g, const KParams &kp, const Range &bound, const LapPart *parts,
+                        int np, int32_t *d_score, uint32_t *d_err) {
+  const bool f16 = use_f16(kp, bound);
+  const PencilArgs pa = make_args(kp, f16);
+  return lap_launch_split(g, f16, pa.sop != 0, pa, parts, np, d_score, d_err);
+}
 #undef TSA_SHAPES
 #undef TSA_ARITH
 

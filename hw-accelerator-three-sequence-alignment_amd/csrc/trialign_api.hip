@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -18,6 +19,7 @@
 
 #include "tsa_internal.h"
 #include "pencil_kernel.h"
+#include "lap_kernel.h"
 
 #ifndef TSA_GIT_DESCRIBE
 #define TSA_GIT_DESCRIBE "dev"
@@ -457,6 +459,112 @@ int tsa_score_batch(const uint8_t *seqs, const int64_t *offsets, int32_t n, cons
   for (auto &t : th) t.join();
   for (int r : rcs) if (r) return r;
   return TSA_OK;
+}
+
+int tsa_score_gpu_multi(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
+                        const uint8_t *c, int32_t lc, const tsa_params *p, const int32_t *devices,
+                        int32_t n_devices, int32_t *score, double *wall_us) {
+  using namespace tsa;
+  if (!score || !devices || n_devices < 1 || n_devices > 64) return TSA_EINVAL;
+  int rc = tsa_validate(a, la, b, lb, c, lc, p);
+  if (rc) return rc;
+  const int nd = tsa_device_count();
+  if (nd <= 0) return TSA_ENODEV;
+  for (int32_t i = 0; i < n_devices; ++i)
+    if (devices[i] < 0 || devices[i] >= nd) return TSA_ENODEV;
+  if (!pencil_exact(p, la, lb, lc)) return TSA_ERANGE;  // the factored form, exact a priori
+  KParams kp;
+  if ((rc = build_kparams(p, &kp))) return rc;
+  const Range bound = value_bound(p, la, lb, lc);
+  const LapGeom g = pencil_split_geom(la, lb, lc, kp, bound, n_devices);
+  if (!g.ok) return TSA_ERANGE;  // no lap schedule, or fewer laps than parts
+  const int np = n_devices;
+  const size_t ws_bytes = lap_workspace_bytes(g);
+  const int64_t off[4] = {0, la, (int64_t)la + lb, (int64_t)la + lb + lc};
+  std::vector<LapPart> parts((size_t)np);
+  std::vector<void *> ws((size_t)np, nullptr);
+  int32_t *d_score = nullptr;
+  uint32_t *d_err = nullptr;
+  int32_t h_score = 0;
+  double t0 = 0, t1 = 0;
+  auto now_us = [] {
+    return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count() * 1e-3;
+  };
+  for (int i = 0; i < np; ++i) parts[i] = LapPart{devices[i], nullptr, 0, 0, nullptr, nullptr, nullptr};
+  // peer access between the distinct devices (each part writes into its
+  // neighbours' workspaces, every part into the last one's error word)
+  for (int i = 0; i < np; ++i)
+    for (int j = 0; j < np; ++j) {
+      const int di = devices[i], dj = devices[j];
+      if (di == dj) continue;
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, di, dj) != hipSuccess || !can) { rc = TSA_EDEVICE; goto done; }
+      HIPCHK(hipSetDevice(di));
+      const hipError_t e = hipDeviceEnablePeerAccess(dj, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) { rc = TSA_EDEVICE; goto done; }
+      (void)hipGetLastError();
+    }
+  for (int i = 0; i < np; ++i) {
+    LapPart &q = parts[i];
+    q.L0 = (int32_t)((int64_t)g.G * i / np);
+    q.L1 = (int32_t)((int64_t)g.G * (i + 1) / np);
+    HIPCHK(hipSetDevice(q.device));
+    HIPCHK(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
+    uint8_t *ds = nullptr;
+    int64_t *dof = nullptr;
+    // fine-grained: its neighbours' stores land here and are polled here
+    if (hipMalloc(&ds, (size_t)off[3]) != hipSuccess || hipMalloc(&dof, sizeof(off)) != hipSuccess ||
+        hipExtMallocWithFlags(&ws[i], ws_bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+      if (ds) (void)hipFree(ds);
+      if (dof) (void)hipFree(dof);
+      rc = TSA_ENOMEM;
+      goto done;
+    }
+    q.d_seqs = ds;
+    q.d_offsets = dof;
+    q.d_ws = ws[i];
+    HIPCHK(hipMemcpyAsync(ds, a, la, hipMemcpyHostToDevice, q.stream));
+    HIPCHK(hipMemcpyAsync(ds + la, b, lb, hipMemcpyHostToDevice, q.stream));
+    HIPCHK(hipMemcpyAsync(ds + la + lb, c, lc, hipMemcpyHostToDevice, q.stream));
+    HIPCHK(hipMemcpyAsync(dof, off, sizeof(off), hipMemcpyHostToDevice, q.stream));
+    HIPCHK(hipMemsetAsync(ws[i], 0, ws_bytes, q.stream));
+    if (i == np - 1) {
+      if (hipMalloc(&d_score, sizeof(int32_t)) != hipSuccess) { rc = TSA_ENOMEM; goto done; }
+      d_err = lap_err_word(g, 1, ws[i]);
+    }
+  }
+  // every workspace is initialised before any part may store into it
+  for (int i = 0; i < np; ++i) {
+    HIPCHK(hipSetDevice(parts[i].device));
+    HIPCHK(hipStreamSynchronize(parts[i].stream));
+  }
+  t0 = now_us();
+  rc = pencil_launch_split(g, kp, bound, parts.data(), np, d_score, d_err);
+  if (rc) goto done;
+  for (int i = 0; i < np; ++i) {
+    HIPCHK(hipSetDevice(parts[i].device));
+    HIPCHK(hipStreamSynchronize(parts[i].stream));
+  }
+  t1 = now_us();
+  HIPCHK(hipSetDevice(parts[np - 1].device));
+  HIPCHK(hipMemcpy(&h_score, d_score, sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (h_score == TSA_SCORE_INVALID) {  // a hand-off timed out: no silent score
+    rc = TSA_EINTERNAL;
+    goto done;
+  }
+  *score = h_score;
+  if (wall_us) *wall_us = t1 - t0;
+done:
+  for (int i = 0; i < np; ++i) {
+    (void)hipSetDevice(parts[i].device);
+    if (parts[i].d_seqs) (void)hipFree((void *)parts[i].d_seqs);
+    if (parts[i].d_offsets) (void)hipFree((void *)parts[i].d_offsets);
+    if (ws[i]) (void)hipFree(ws[i]);
+    if (i == np - 1 && d_score) (void)hipFree(d_score);
+    if (parts[i].stream) (void)hipStreamDestroy(parts[i].stream);
+  }
+  return rc;
 }
 
 int tsa_align_gpu(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb, const uint8_t *c,

@@ -158,6 +158,24 @@ int tsa_score_batch_async_p2(const uint8_t *d_packed, const int64_t *d_offsets,
  * hold (n + 3) / 4 bytes. TSA_EINVAL on a symbol above 4. Host only. */
 int tsa_pack2(const uint8_t *syms, int64_t n, uint8_t *out);
 
+/* Score ONE triple with its cube split over several GPUs (synchronous): the
+ * reference's slicing of the (y,z) plane into pencils chained through face
+ * SRAMs (src/TriAlign_1cyc.v:78-98,127-140, pic/Memory.png), distributed --
+ * the cube's laps (2*NW rows of y each) are cut into
+ * n_devices contiguous runs, part i on devices[i]; the last lap of part i
+ * hands its y records to part i+1 by system-scope stores into part i+1's
+ * fine-grained workspace over xGMI (peer access is enabled between the listed
+ * devices). A device may be listed more than once: its parts then run as
+ * concurrent launches on separate streams of that device. Requires the
+ * factored form to be exact a priori (else TSA_ERANGE) and at least n_devices
+ * laps (TSA_ERANGE). A timed-out hand-off returns TSA_EINTERNAL (never a
+ * silent score). wall_us (nullable): host wall time from the first launch to
+ * the last part's completion. */
+int tsa_score_gpu_multi(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
+                        const uint8_t *c, int32_t lc, const tsa_params *p,
+                        const int32_t *devices, int32_t n_devices, int32_t *score,
+                        double *wall_us);
+
 /* Optimal alignment of one triple (synchronous, HIP device `device`): the
  * path behind the score, as one move per alignment column. This has no RTL
  * counterpart -- the testbench's alignment-output ports are commented out

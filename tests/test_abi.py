@@ -134,6 +134,9 @@ def test_no_cpu_fallback_without_gpu(tsa):
     with pytest.raises(tsa.TsaError) as e:
         tsa.score_batch([([0], [1], [2])])
     assert e.value.rc == tsa.TSA_ENODEV
+    with pytest.raises(tsa.TsaError) as e:
+        tsa.score_multi([0] * 64, [0] * 64, [0] * 64, [0, 1])
+    assert e.value.rc == tsa.TSA_ENODEV
 
 
 def test_cli_reports_no_device_or_score():

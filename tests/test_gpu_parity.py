@@ -564,3 +564,59 @@ def test_packed2_input_matches_bytes(gpu, orc, kernel):
             torch.cuda.synchronize()
             out.append(d_sc.cpu().numpy())
         assert np.array_equal(out[0], ref) and np.array_equal(out[1], ref), (kernel, n, L)
+
+
+# ---- one cube split over devices by laps (tsa_score_gpu_multi)
+@pytest.mark.parametrize("L,parts", [(64, 2), (128, 2), (256, 2), (256, 4), (512, 3)])
+def test_split_cube_matches_oracle(gpu, orc, synth, L, parts):
+    """The cube's laps cut into `parts` contiguous runs, each its own launch
+    with its own fine-grained workspace, handing y records to the next by
+    system-scope stores -- on one box the parts share device 0 (concurrent
+    launches on separate streams), which runs the same protocol as the
+    multi-GPU case minus the xGMI hop. Must equal the literal oracle."""
+    a, b, c = synth.triple(40 + L + parts, L)
+    got, wall = gpu.score_multi(a, b, c, [0] * parts)
+    assert got == orc.score(a, b, c)
+    assert wall > 0
+
+
+@pytest.mark.parametrize("kind", ["all_a", "all_mismatch", "related"])
+def test_split_cube_extremes(gpu, orc, synth, monkeypatch, kind):
+    """Seam cases across the part boundary: the optimum of all-A runs down the
+    diagonal through every boundary lap; all-mismatch sits at the low bound."""
+    L = 192
+    if kind == "all_a":
+        a = b = c = np.zeros(L, np.uint8)
+    elif kind == "all_mismatch":
+        a, b, c = (np.full(L, v, np.uint8) for v in (0, 1, 2))
+    else:
+        a, b, c = synth.related_triple(7, L)
+    got, _ = gpu.score_multi(a, b, c, [0, 0])
+    assert got == orc.score(a, b, c), kind
+    if kind == "all_a":
+        assert got == 3 * L
+
+
+def test_split_cube_int16_and_ragged(gpu, orc, synth):
+    """Ragged lengths (lap and tile counts not multiples of the part count) and
+    the int16 form (match 5 with 16-bit words: the bound leaves the exact-f16
+    range at 150^3)."""
+    a, b, c = synth.triple(3, 150)
+    b, c = b[:101], c[:77]
+    assert gpu.score_multi(a, b, c, [0, 0, 0])[0] == orc.score(a, b, c)
+    kw = dict(match=5, mismatch=-4, gap_open=10, gap_extend=1, score_bits=16)
+    a, b, c = synth.triple(9, 150)
+    got = gpu.score_multi(a, b, c, [0, 0], gpu.TsaParams.default(**kw))[0]
+    assert got == orc.score(a, b, c, orc.default_params(**kw))
+
+
+def test_split_cube_errors(gpu, synth):
+    """Fewer laps than parts, bad device ids and a non-exact parameter set are
+    refused with the reference-style error codes, never a silent score."""
+    a, b, c = synth.triple(1, 16)
+    with pytest.raises(gpu.TsaError) as e:
+        gpu.score_multi(a, b, c, [0] * 8)   # 16 rows = 2 laps < 8 parts
+    assert e.value.rc == gpu.TSA_ERANGE
+    with pytest.raises(gpu.TsaError) as e:
+        gpu.score_multi(a, b, c, [gpu.device_count()])
+    assert e.value.rc == gpu.TSA_ENODEV
