@@ -424,7 +424,24 @@ def time_singles(args, tsa, synth, hot, dev, L, params):
             out["configs[3]: 1024^3 (12-bit RTL words, checked)"] = r
     except Exception as e:  # noqa: BLE001
         log("single-cube measurement failed:", e)
+    if not args.no_extra_configs:
+        out["split over devices"] = time_split(world_devices=args.gpus)
     return out
+
+
+def time_split(world_devices: int) -> dict:
+    """One cube split over devices by laps, in a child
+    process with its own time limit: 2 parts sharing device 0 at N = 1,
+    devices 0..N-1 on an N-GPU run (rank 0, while the other ranks wait)."""
+    devs = ",".join(str(d) for d in range(world_devices)) if world_devices > 1 else "0,0"
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "split_cube.py"), "--devices", devs]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
+        if r.returncode == 0 and r.stdout.strip():
+            return json.loads(r.stdout.strip().splitlines()[-1])
+        return {"devices": devs, "error": f"rc={r.returncode}: {r.stderr.strip()[-300:]}"}
+    except Exception as e:  # noqa: BLE001
+        return {"devices": devs, "error": str(e)[-300:]}
 
 
 def oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single):
