@@ -69,6 +69,9 @@ namespace tsa {
 #ifndef TSA_LAP_PD4
 #define TSA_LAP_PD4 3
 #endif
+#ifndef TSA_LAP_DELAY  // loader start lag behind the producers (steps), see the loader
+#define TSA_LAP_DELAY 0
+#endif
 __host__ __device__ constexpr int lap_pd(int M) {
   return M == 1 ? TSA_LAP_PD1 : M == 2 ? TSA_LAP_PD2 : TSA_LAP_PD4;
 }
@@ -551,6 +554,25 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       }
     }
     __syncthreads();  // (matches the compute waves' prologue barrier)
+#if TSA_LAP_DELAY > 0
+    // Start the prefetch window TSA_LAP_DELAY steps behind the producers'
+    // frontier: wait until the records that far ahead are stored, so a window
+    // deeper than the frontier allows (LPD) fetches stored records instead of
+    // stale ones -- the loader then delivers LPD records per round trip.
+    {
+      Fetch f;
+      const int32_t dy = min(TSA_LAP_DELAY, T_above - YOFF - 1);
+      if (yin && dy > 0) {
+        fetch_y(dy, f);
+        if (!y_ok(dy, f)) settle_y(dy, f);
+      }
+      const int32_t dz = min(ZT + ZA + TSA_LAP_DELAY, T_left - 1);
+      if (zin && dz >= ZT + ZA) {
+        fetch_z(dz, f);
+        if (!z_ok(dz, f)) settle_z(dz, f);
+      }
+    }
+#endif
     Fetch fq[LPD];
 #pragma unroll
     for (int j = 0; j < LPD; ++j) fetch(j, fq[j]);
