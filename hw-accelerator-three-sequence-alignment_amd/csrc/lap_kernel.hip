@@ -1069,6 +1069,8 @@ static double lap_step_us(int M, int NW, int64_t wg_per_cu) {
 
 LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW,
                  bool full_rings, bool f16, bool sop) {
+  // A/B knob: full-length rings (no back-pressure) on every lap launch
+  if (const char *e = getenv("TSA_LAP_FULL_RINGS")) full_rings = full_rings || atoi(e) != 0;
   LapGeom g{};
   g.M = M;
   g.NW = NW;
@@ -1080,8 +1082,14 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   const int YOFF = 2 * (NW - 1) + 1;  // lap lag of a record (kernel: YOFF)
   const int32_t T = max_la + YOFF + ZT;  // >= every workgroup's step count
   auto pow2 = [](int64_t v) { int64_t p = 1; while (p < v) p <<= 1; return (int32_t)p; };
-  g.YR = full_rings ? pow2(T) : pow2(YOFF + LPD + 48);
-  g.ZR = full_rings ? pow2(T) : pow2(ZT + LPD + 48);
+  // ring slots beyond the natural lag: beyond 512 per side the lag between
+  // neighbours drifts further (more laps and tiles behind them) and 48 slots
+  // made producers wait (1024^3: 1235 back-pressure waits, 3.30 ms; 240 slots:
+  // 34 waits, 3.06 ms, 580 MB). A/B knob TSA_LAP_RING_SLACK.
+  int slack = std::max(max_la, std::max(max_lb, max_lc)) > 512 ? 240 : 48;
+  if (const char *e = getenv("TSA_LAP_RING_SLACK")) slack = std::max(16, atoi(e));
+  g.YR = full_rings ? pow2(T) : pow2(YOFF + LPD + slack);
+  g.ZR = full_rings ? pow2(T) : pow2(ZT + LPD + slack);
   g.lds = lap_lds_bytes(M, NW, max_la);
   if (const char *e = getenv("TSA_LAP_LDS_EXTRA")) g.lds += (size_t)atoi(e);  // diagnostic knob
   const int64_t wgs = (int64_t)n * g.G * g.GZ;
