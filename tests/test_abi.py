@@ -173,3 +173,14 @@ def test_align_argument_checks(tsa):
     # traceback helpers are host-only
     assert tsa.path_score([0] * 4, [0] * 4, [0] * 4, (0, 0, 0), [0] * 4) == 12
     assert tsa.render_alignment("ACGT", "AGT", "ACT", (0, 0, 0), [0, 6, 4, 0]) == ("ACGT", "A-GT", "AC-T")
+
+
+def test_split_cube_argument_checks(tsa):
+    """tsa_score_gpu_multi validates before touching a device: an empty device
+    list or a bad symbol is TSA_EINVAL on any host."""
+    with pytest.raises(tsa.TsaError) as e:
+        tsa.score_multi([0] * 8, [0] * 8, [0] * 8, [])
+    assert e.value.rc == tsa.TSA_EINVAL
+    with pytest.raises(tsa.TsaError) as e:
+        tsa.score_multi([0, 7], [0] * 8, [0] * 8, [0, 0])
+    assert e.value.rc == tsa.TSA_EINVAL
