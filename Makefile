@@ -3,9 +3,11 @@
 PKG      := hw-accelerator-three-sequence-alignment_amd
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
-GITDESC  := $(shell git describe --always --dirty 2>/dev/null || echo nogit)
-HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function \
-            -DTSA_GIT_DESCRIBE='"$(GITDESC)"'
+# hash of csrc/*.{hip,h} + include/trialign.h, baked into tsa_version() so a
+# run can name the sources its binary came from (srchash.py; the tests and the
+# bench rebuild a library whose hash is not the tree's)
+SRC_HASH := $(shell python3 $(PKG)/srchash.py)
+HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function
 LIB      := $(PKG)/lib/libtrialign.so
 CLI      := $(PKG)/bin/tsa
 SRCS     := $(wildcard $(PKG)/csrc/*.hip)
@@ -21,6 +23,10 @@ all: $(LIB) $(CLI) oracle
 $(PKG)/build/%.o: $(PKG)/csrc/%.hip $(HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# the version string lives in trialign_api.o: rebuild it whenever any source changes
+$(PKG)/build/trialign_api.o: $(SRCS) $(PKG)/srchash.py
+$(PKG)/build/trialign_api.o: HIPFLAGS += -DTSA_SRC_HASH='"$(SRC_HASH)"'
 
 $(LIB): $(OBJS)
 	@mkdir -p $(dir $@)

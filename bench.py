@@ -164,7 +164,8 @@ def parse_args(argv=None):
                     help="skip the single-cube timings other than configs[2]")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target wall time of the CPU-baseline sample")
-    ap.add_argument("--check", type=int, default=4, help="triples checked vs the oracle")
+    ap.add_argument("--check", type=int, default=16,
+                    help="batch triples checked vs the oracle (both ends included); 0 = no parity leg")
     ap.add_argument("--score-bits", type=int, default=12,
                     help="12 = RTL wrap (default); 16/0 for cubes beyond the RTL envelope (1024^3)")
     return ap.parse_args(argv)
@@ -331,12 +332,16 @@ def report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gc
     roofline.update({"kernel": kernel_name, "kernel_ms_per_step": round(kernel_ms_per_step, 4),
                      "hbm": hbm, "hbm_model": hbm_model, "pmc_stale": pmc.get("stale")})
 
+    # the single cubes' oracle scores (two 1024^3 among them, ~30 s each on
+    # one core) run in threads while the GPU times the cubes
+    pending = start_single_oracles(args, synth, L) if extras and args.check > 0 else None
     single = {}
     if extras:
         single = time_singles(args, tsa, synth, hot, dev, L, params)
     parity, cpu_baseline = None, None
     if extras and args.check > 0:
-        parity, cpu_baseline = oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single)
+        parity, cpu_baseline = oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single,
+                                          pending)
 
     return {
         "metric": "GCUPS (10^9 3D-DP cell updates/s), 256^3 cubes",
@@ -365,14 +370,30 @@ def report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gc
         "cpu_baseline": cpu_baseline,
         "single_cube": single,
         "parity": parity,
+        "build": tsa.build_info(),
     }
 
 
+def single_specs(args, L):
+    """(key, length, score_bits, reps, kernel) of every single cube rank 0
+    times: configs[2] (L^3, the batch's words), configs[1] (64^3), the
+    paper's 128^3 and 512^3 (Table III, RTL 12-bit words) and configs[3]
+    (1024^3 with 16-bit words, and with the RTL's 12-bit words on the checked
+    kernel)."""
+    specs = [(f"configs[2]: {L}^3", L, args.score_bits, 7, None)]
+    if not args.no_extra_configs:
+        specs += [("configs[1]: 64^3", 64, args.score_bits, 15, None),
+                  ("paper N=128: 128^3", 128, args.score_bits, 9, None),
+                  ("paper N=512: 512^3", 512, args.score_bits, 5, None),
+                  ("configs[3]: 1024^3 (16-bit words)", 1024, 16, 5, None),
+                  # the score is exact, or TSA_SCORE_UNCERTIFIED (then rescored by PLANE)
+                  ("configs[3]: 1024^3 (12-bit RTL words, checked)", 1024, 12, 5, "checked")]
+    return specs
+
+
 def time_singles(args, tsa, synth, hot, dev, L, params):
-    """Single-cube latency: configs[2] (L^3, params as the batch), configs[1]
-    (64^3), the paper's 128^3 and 512^3 (Table III, RTL 12-bit words) and
-    configs[3] (1024^3, 16-bit words: beyond the RTL envelope). Median of
-    individually timed calls on the launch stream (a latency)."""
+    """Single-cube latency (single_specs): median of individually timed calls
+    on the launch stream. Each cube is synth.triple(0, length)."""
     import torch
     stream = hot.stream
 
@@ -406,24 +427,17 @@ def time_singles(args, tsa, synth, hot, dev, L, params):
         if Ls in ASIC_MS and prm.score_bits == 12:
             r["asic_ms"] = ASIC_MS[Ls]
             r["vs_asic"] = round(ASIC_MS[Ls] / sms, 3)
+        if kernel == "checked":
+            r["certified"] = r["score"] != tsa.SCORE_UNCERTIFIED
         return r
 
     out = {}
-    try:
-        out[f"configs[2]: {L}^3"] = one(L, params, 7)
-        if not args.no_extra_configs:
-            out["configs[1]: 64^3"] = one(64, params, 15)
-            out["paper N=128: 128^3"] = one(128, params, 9)
-            out["paper N=512: 512^3"] = one(512, params, 5)
-            out["configs[3]: 1024^3 (16-bit words)"] = one(
-                1024, tsa.TsaParams.default(score_bits=16), 5)
-            # the RTL's own 12-bit words at 1024^3: the checked lap kernel
-            # (the score is exact, or TSA_SCORE_UNCERTIFIED and rescored by PLANE)
-            r = one(1024, params, 5, kernel="checked")
-            r["certified"] = r["score"] != tsa.SCORE_UNCERTIFIED
-            out["configs[3]: 1024^3 (12-bit RTL words, checked)"] = r
-    except Exception as e:  # noqa: BLE001
-        log("single-cube measurement failed:", e)
+    for key, Ls, bits, reps, kernel in single_specs(args, L):
+        try:
+            out[key] = one(Ls, tsa.TsaParams.default(score_bits=bits), reps, kernel)
+        except Exception as e:  # noqa: BLE001  (recorded; the parity leg counts it)
+            log(f"single-cube {key} failed:", e)
+            out[key] = {"error": str(e)[-300:], "score_bits": bits}
     if not args.no_extra_configs:
         out["split over devices"] = time_split(world_devices=args.gpus)
     return out
@@ -444,26 +458,92 @@ def time_split(world_devices: int) -> dict:
         return {"devices": devs, "error": str(e)[-300:]}
 
 
-def oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single):
-    """Checker + CPU baseline (the only use of oracle/ here): a sample of the
-    gathered scores vs the C oracle, and at N=1 the oracle timed on a bounded
-    sample of the same workload on every host core the job may use."""
-    parity, cpu_baseline = None, None
+def _import_oracle():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402
+    return oracle
+
+
+def start_single_oracles(args, synth, L):
+    """Oracle scores of every single cube bench times (and splits), keyed by
+    (length, score_bits), started in threads (the C oracle releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
     try:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle  # noqa: E402
+        oracle = _import_oracle()
+    except Exception as e:  # noqa: BLE001
+        log("oracle unavailable:", e)
+        return None
+    want = sorted({(Ls, bits) for _, Ls, bits, _, _ in single_specs(args, L)}, key=lambda t: -t[0])
+    if not args.no_extra_configs:  # the split child process times 256^3 (12-bit) and 1024^3 (16-bit)
+        want = sorted(set(want) | {(256, 12), (1024, 16)}, key=lambda t: -t[0])
+    pool = ThreadPoolExecutor(max_workers=max(1, min(len(want), host_cores())))
+    futs = {(Ls, bits): pool.submit(lambda Ls=Ls, bits=bits: oracle.score(
+        *synth.triple(0, Ls), oracle.default_params(score_bits=bits))) for Ls, bits in want}
+    pool.shutdown(wait=False)
+    return futs
+
+
+def oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single, pending):
+    """Checker + CPU baseline (the only use of oracle/ here).
+
+    parity: >= args.check gathered batch scores (both ends included), every
+    single cube rank 0 timed and both split-cube scores against the C oracle
+    on the same inputs, plus the reference's dat triple through tsa_score_gpu
+    (golden score 1, tests/golden/golden.json). Each config is listed as
+    {gpu, oracle, ok}; parity["mismatches"] counts every failure (an error or
+    a missing score counts too) and main() exits non-zero when it is not 0.
+    cpu_baseline: at N=1 the oracle timed on a bounded sample of the same
+    workload on every host core the job may use."""
+    parity, cpu_baseline = {"mismatches": 1, "error": "oracle leg did not run"}, None
+    try:
+        oracle = _import_oracle()
         cores = host_cores()
+        configs = {}
+
+        def put(name, gpu, ref):
+            configs[name] = {"gpu": gpu, "oracle": ref, "ok": gpu is not None and gpu == ref}
+
+        # batch: both ends + an even spread
         idx = sorted(set([0, n_total - 1] + [int(v) for v in np.linspace(0, n_total - 1, args.check)]))
         trip = [synth.triple(i, L) for i in idx]
         cs, co = tsa.pack_batch(trip)
         oparams = oracle.default_params(score_bits=args.score_bits)
         ref = oracle.score_batch(cs, co, oparams, nthreads=cores)
         got = all_scores[idx]
-        parity = {"checked": len(idx), "mismatches": int((ref != got).sum()),
-                  "against": "oracle/tsa_oracle.c"}
-        key = f"configs[2]: {L}^3"
-        if key in single:
-            parity["single_cube_ok"] = bool(single[key]["score"] == int(ref[0]))
+        bad = [int(i) for i, g, r in zip(idx, got, ref) if g != r]
+        batch = {"checked": len(idx), "indices": [int(i) for i in idx], "mismatches": len(bad),
+                 "mismatched_indices": bad, "score_bits": args.score_bits}
+        # single cubes and the split (oracle scores started before the GPU timings)
+        refs = {k: f.result() for k, f in pending.items()} if pending else {}
+        for key, Ls, bits, _, _ in single_specs(args, L):
+            r = single.get(key, {})
+            put(key, r.get("score"), refs.get((Ls, bits)))
+        sp = single.get("split over devices")
+        if isinstance(sp, dict):
+            lens = [k for k in sp if k.endswith("^3")]
+            if not lens:
+                put("split over devices", None, None)
+            for k in lens:
+                Ls = int(k[:-2])
+                for part in ("one_part", "split"):
+                    put(f"split over devices {sp.get('devices')}: {k} {part}",
+                        sp[k].get(part, {}).get("score"), refs.get((Ls, sp[k]["score_bits"])))
+        # the reference's own parity input: dat/{A,B,C}_seq.dat through tsa_score_gpu
+        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+            dat = next(c for c in json.load(f)["cases"] if c["name"] == "dat")
+        try:
+            g_dat = tsa.score(dat["a"], dat["b"], dat["c"], device=0)
+        except Exception as e:  # noqa: BLE001
+            log("dat triple failed:", e)
+            g_dat = None
+        put("configs[0]: dat/{A,B,C}_seq.dat (tsa_score_gpu)", g_dat,
+            oracle.score(dat["a"], dat["b"], dat["c"]))
+        configs["configs[0]: dat/{A,B,C}_seq.dat (tsa_score_gpu)"]["golden"] = dat["score"]
+        if dat["score"] != configs["configs[0]: dat/{A,B,C}_seq.dat (tsa_score_gpu)"]["oracle"]:
+            configs["configs[0]: dat/{A,B,C}_seq.dat (tsa_score_gpu)"]["ok"] = False
+        n_bad = len(bad) + sum(not c["ok"] for c in configs.values())
+        parity = {"mismatches": n_bad, "batch": batch, "configs": configs,
+                  "against": "oracle/tsa_oracle.c (literal RTL form, same inputs)"}
         if world == 1 and not args.no_cpu_baseline:
             # bounded sample of the same workload: one L^3 triple per thread per round
             t_one = oracle.now()
@@ -486,6 +566,7 @@ def oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single):
             }
     except Exception as e:  # noqa: BLE001
         log("oracle leg failed:", e)
+        parity = {"mismatches": 1, "error": str(e)[-300:]}
     return parity, cpu_baseline
 
 
@@ -511,6 +592,10 @@ def main(argv=None):
     rec = run_rank(args, world, rank, local_rank, "nccl", GpuBatch)
     if rec is not None:
         print(json.dumps(rec), flush=True)
+        par = rec.get("parity")
+        if par is not None and par.get("mismatches", 0) != 0:
+            log(f"bench.py: {par['mismatches']} parity failure(s) against the oracle")
+            sys.exit(3)
 
 
 if __name__ == "__main__":

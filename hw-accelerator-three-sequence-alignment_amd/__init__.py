@@ -168,7 +168,22 @@ def lib() -> ctypes.CDLL:
 
 
 def version() -> str:
+    """tsa_version(): "trialign-mi355x gfx950 src=<hash>" -- the hash of the
+    sources the loaded binary was built from (srchash.py)."""
     return _lib.tsa_version().decode()
+
+
+def source_hash() -> str:
+    """Hash of the library sources in this tree (srchash.py)."""
+    from . import srchash
+    return srchash.source_hash()
+
+
+def build_info() -> dict:
+    """Which binary is loaded and whether it was built from this tree."""
+    v = version()
+    tree = source_hash()
+    return {"version": v, "lib": LIB_PATH, "tree_src": tree, "current": v.endswith("src=" + tree)}
 
 
 def device_count() -> int:

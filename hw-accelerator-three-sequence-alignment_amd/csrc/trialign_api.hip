@@ -21,8 +21,8 @@
 #include "pencil_kernel.h"
 #include "lap_kernel.h"
 
-#ifndef TSA_GIT_DESCRIBE
-#define TSA_GIT_DESCRIBE "dev"
+#ifndef TSA_SRC_HASH  // set by the Makefile: srchash.py over csrc/*.{hip,h} + include/trialign.h
+#define TSA_SRC_HASH "unhashed"
 #endif
 
 namespace tsa {
@@ -161,7 +161,7 @@ const char *tsa_strerror(int rc) {
   }
 }
 
-const char *tsa_version(void) { return "trialign-mi355x gfx950 " TSA_GIT_DESCRIBE; }
+const char *tsa_version(void) { return "trialign-mi355x gfx950 src=" TSA_SRC_HASH; }
 
 int tsa_device_count(void) {
   int n = 0;

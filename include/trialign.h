@@ -226,7 +226,9 @@ int tsa_device_count(void);
 /* Short description of a return code. */
 const char *tsa_strerror(int rc);
 
-/* Library build id, e.g. "trialign-mi355x gfx950 <git-describe>". */
+/* Library build id, "trialign-mi355x gfx950 src=<hash>": the first 16 hex
+ * digits of a SHA-256 over the library's sources (csrc .hip and .h files and
+ * this header; srchash.py), so a run names the sources its binary came from. */
 const char *tsa_version(void);
 
 #ifdef __cplusplus

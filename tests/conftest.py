@@ -20,11 +20,26 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP device (MI355X); runs the HIP kernels")
 
 
+def _srchash():
+    spec = importlib.util.spec_from_file_location("tsa_srchash", os.path.join(PKG_DIR, "srchash.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def _ensure_built():
+    """Build when the library is missing or was built from other sources
+    than this tree's (the hash tsa_version() carries, srchash.py)."""
     lib = os.path.join(PKG_DIR, "lib", "libtrialign.so")
     orc = os.path.join(ROOT, "oracle", "_build", "libtsa_oracle.so")
-    if not (os.path.exists(lib) and os.path.exists(orc)):
+    if not (os.path.exists(lib) and os.path.exists(orc) and _srchash().is_current(lib)):
         subprocess.run(["make", "-s", "-j8"], cwd=ROOT, check=True)
+
+
+def pytest_report_header(config):
+    h = _srchash()
+    lib = os.path.join(PKG_DIR, "lib", "libtrialign.so")
+    return [f"trialign sources src={h.source_hash()}; libtrialign.so built from src={h.built_hash(lib)}"]
 
 
 def load_pkg():
