@@ -208,7 +208,12 @@ def _as_u8(seq) -> np.ndarray:
             seq = [SYMBOLS[ch] for ch in seq.upper()]
         except KeyError as e:
             raise TsaError(TSA_EINVAL, f"symbol {e}") from None
-    arr = np.ascontiguousarray(np.asarray(seq, dtype=np.uint8))
+    src = np.asarray(seq)
+    if src.dtype != np.uint8:
+        # no silent wrap into a valid symbol (256 -> 0 = 'A', -1 -> 255)
+        if src.size and (src.dtype.kind not in "iub" or int(src.min()) < 0 or int(src.max()) > 255):
+            raise TsaError(TSA_EINVAL, "symbols must be integers 0..4")
+    arr = np.ascontiguousarray(src, dtype=np.uint8)
     if arr.ndim != 1:
         raise TsaError(TSA_EINVAL, "sequence must be 1-D")
     return arr
@@ -425,7 +430,7 @@ def pack2(seqs) -> np.ndarray:
     """Symbols (0..4) -> 2-bit packed bytes, four per byte, symbol i at bits
     2(i%4) of byte i/4 (tsa_pack2; N = 4 packs as A, as the RTL's 2-bit
     registers hold it)."""
-    s = np.ascontiguousarray(_as_u8(seqs) if not isinstance(seqs, np.ndarray) else seqs, dtype=np.uint8)
+    s = _as_u8(seqs)
     out = np.zeros(max((len(s) + 3) // 4, 1), dtype=np.uint8)
     _check(_lib.tsa_pack2(_ptr(s, ctypes.c_uint8), len(s), _ptr(out, ctypes.c_uint8)), "tsa_pack2")
     return out[: (len(s) + 3) // 4]

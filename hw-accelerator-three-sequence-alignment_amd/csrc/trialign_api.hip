@@ -487,6 +487,7 @@ int tsa_score_gpu_multi(const uint8_t *a, int32_t la, const uint8_t *b, int32_t 
   uint32_t *d_err = nullptr;
   int32_t h_score = 0;
   double t0 = 0, t1 = 0;
+  bool launched = false;
   auto now_us = [] {
     return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
                std::chrono::steady_clock::now().time_since_epoch()).count() * 1e-3;
@@ -540,6 +541,7 @@ int tsa_score_gpu_multi(const uint8_t *a, int32_t la, const uint8_t *b, int32_t 
     HIPCHK(hipStreamSynchronize(parts[i].stream));
   }
   t0 = now_us();
+  launched = true;
   rc = pencil_launch_split(g, kp, bound, parts.data(), np, d_score, d_err);
   if (rc) goto done;
   for (int i = 0; i < np; ++i) {
@@ -556,6 +558,15 @@ int tsa_score_gpu_multi(const uint8_t *a, int32_t la, const uint8_t *b, int32_t 
   *score = h_score;
   if (wall_us) *wall_us = t1 - t0;
 done:
+  // once any part may be running, every part's stream drains before any
+  // allocation goes: a part on another device can still be storing into its
+  // neighbours' workspaces (hipFree only synchronises its own device)
+  if (launched)
+    for (int i = 0; i < np; ++i)
+      if (parts[i].stream) {
+        (void)hipSetDevice(parts[i].device);
+        (void)hipStreamSynchronize(parts[i].stream);
+      }
   for (int i = 0; i < np; ++i) {
     (void)hipSetDevice(parts[i].device);
     if (parts[i].d_seqs) (void)hipFree((void *)parts[i].d_seqs);

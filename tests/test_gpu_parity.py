@@ -620,3 +620,39 @@ def test_split_cube_errors(gpu, synth):
     with pytest.raises(gpu.TsaError) as e:
         gpu.score_multi(a, b, c, [gpu.device_count()])
     assert e.value.rc == gpu.TSA_ENODEV
+    # the a-priori bound of a 1024^3 cube leaves the RTL's 12-bit word: the
+    # split (factored form, exact a priori only) refuses it
+    a, b, c = synth.triple(1, 1024)
+    with pytest.raises(gpu.TsaError) as e:
+        gpu.score_multi(a, b, c, [0, 0], gpu.TsaParams.default(score_bits=12))
+    assert e.value.rc == gpu.TSA_ERANGE
+
+
+def test_split_cube_timeout_is_reported_not_silent(gpu, synth, monkeypatch):
+    """Injected hand-off timeout (TSA_LAP_SPIN_LIMIT=0: a consumer's first
+    poll gives up) on the split path: TSA_EINTERNAL, never a score; the next
+    call with the default limit is exact again."""
+    a, b, c = synth.triple(5, 128)
+    monkeypatch.setenv("TSA_LAP_SPIN_LIMIT", "0")
+    with pytest.raises(gpu.TsaError) as e:
+        gpu.score_multi(a, b, c, [0, 0])
+    assert e.value.rc == gpu.TSA_EINTERNAL
+    monkeypatch.delenv("TSA_LAP_SPIN_LIMIT")
+    import oracle
+    assert gpu.score_multi(a, b, c, [0, 0])[0] == oracle.score(a, b, c)
+
+
+@pytest.mark.parametrize("devs", [[0, 1], [0, 1, 1], [1, 0]])
+def test_split_cube_across_devices(gpu, orc, synth, devs):
+    """The real multi-GPU split: peer access, fine-grained rings on distinct
+    devices and system-scope hand-offs over xGMI (skipped on a one-GPU box).
+    256^3 and a ragged shape; no fallback may fire."""
+    if gpu.device_count() < 2:
+        pytest.skip("needs two HIP devices")
+    before = (gpu.fallback_count(), gpu.check_fallback_count())
+    a, b, c = synth.triple(11, 256)
+    assert gpu.score_multi(a, b, c, devs)[0] == orc.score(a, b, c)
+    a, b, c = synth.triple(12, 200)
+    b, c = b[:173], c[:131]
+    assert gpu.score_multi(a, b, c, devs)[0] == orc.score(a, b, c)
+    assert (gpu.fallback_count(), gpu.check_fallback_count()) == before

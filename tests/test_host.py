@@ -135,3 +135,10 @@ def test_pack2_layout(tsa):
         assert np.array_equal(back, s & 3)
     with pytest.raises(tsa.TsaError):
         tsa.pack2(np.array([0, 5], np.uint8))
+    # int-typed input must not wrap into a valid symbol (256 -> 0 = 'A')
+    for bad in (np.array([0, 256], np.int64), np.array([1, -1], np.int32), np.array([0.0, 1.0])):
+        with pytest.raises(tsa.TsaError):
+            tsa.pack2(bad)
+        with pytest.raises(tsa.TsaError):
+            tsa.validate(bad, [0], [0])
+    assert list(tsa.pack2(np.array([1, 2, 3, 4], np.int64))) == [0b00111001]
