@@ -47,11 +47,16 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 BYTES_PER_CELL = 28            # 7 int16 states written + read once
 # VALU issue ceiling of the packed-16-bit wave64 instructions the pencil kernel
 # issues: 256 CU x 4 SIMD x 2.4 GHz / 4 cycles per instruction per SIMD. The
-# 4 cycles are measured (tools/valu_peak.hip -> profiles/r1_valu_peak.jsonl:
-# <= 0.24 instr/cycle/SIMD for v_pk_maximum3_f16, v_pk_add_f16, v_bfi_b32, DPP
-# movs at 1-8 waves per SIMD), not the 2-cycle issue of a 32-wide op.
+# 4 cycles are measured (tools/valu_peak.hip -> profiles/r3_valu_peak.jsonl):
+# v_pk_maximum3_f16, v_pk_add_f16, v_pk_fma_f32, v_pk_max_i16, v_bfi_b32,
+# v_perm_b32, DPP movs and v_max_i32 / v_max3_f32 top out at 0.23-0.24
+# instructions per cycle per SIMD at 4-8 waves; the same harness does see the
+# guide's faster issue (MI355X_MICROARCH.md:54,473) on v_add_u32 (0.40-0.43,
+# 2 cycles) and partly on v_fma_f32 (0.28), so 4 cycles is the packed ops'
+# own cost, not a limit of the harness.
 VALU_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 4
-VALU_PEAK_SOURCE = "profiles/r1_valu_peak.jsonl (tools/valu_peak.hip)"
+VALU_PEAK_SOURCE = ("profiles/r3_valu_peak.jsonl (tools/valu_peak.hip: packed-16 ops 0.24 "
+                    "instr/cycle/SIMD; 2-cycle control v_add_u32 0.43; MI355X_MICROARCH.md:54,473)")
 # Paper Table III (pic/Result.png): ASIC runtime per N^3 cube, ms
 ASIC_MS = {64: 0.03, 128: 0.19, 256: 1.39, 512: 10.82}
 
