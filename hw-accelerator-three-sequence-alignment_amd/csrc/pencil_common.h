@@ -68,6 +68,10 @@ struct PencilArgs {
   float dmf;                      // match - mismatch (per-position DMC, exact f16)
   int32_t sop;                  // TSA_S3_SOP
   int32_t packed;               // 2-bit packed input symbols (tsa_sym)
+  // V-space helix (cell_messages_vs): values of cell (x,y,z) shifted by
+  // lam*(x+y+z); lam = GE = -MISMATCH, f16 bits in both halves
+  int32_t lam;                  // lam as an integer (0: not V-space)
+  uint32_t v_lam, v_cP, v_dO;   // lam, GO + MISMATCH + lam, GO - GE
 };
 
 
@@ -336,6 +340,56 @@ __device__ __forceinline__ void cell_messages_f16(
   }
 }
 
+// The same cell in V-space (tests/test_cell_algebra.py replays it against the
+// oracle): every value of cell (x,y,z) is stored shifted by lam*(x+y+z), a
+// potential -- every path into a cell gains the same amount, so no max
+// changes -- with lam = GE = -MISMATCH (the RTL's constants: 1). A transition
+// that advances x+y+z by d then pays lam*d less, so (f16 form, the mismatch
+// folded into the pair messages as above):
+//  * the pair targets' extend penalty GE - MISMATCH - 2 lam vanishes:
+//      Ixy' = max(G_z, best - (GO - GE)),  G_z = max(Ix, Iy, Ixy)  (G_x, G_y alike);
+//  * a single target is the better of its own extension and the two pair
+//    messages that share its gaps (the penalty table is a sum over the gapped
+//    axes, src/PE_1cyc.v:172-194, so max(Ixy', Ixz') covers every other source):
+//      Ix' = max(Ix - lam, max(Ixy', Ixz') - (GO + MISMATCH + lam));
+//  * M adds no constant: 3 MISMATCH + 3 lam = 0 (the SOP form folds 3 lam into K).
+// 25 instructions per pair (RTL) against cell_messages_f16's 33. Zero faces
+// become lam*q at coordinate sum q: the kernel injects those (pencil_kernel.hip).
+template <int M, bool SOP>
+__device__ __forceinline__ void cell_messages_vs(
+    const uint32_t (&a)[M], const uint32_t (&b)[M], const uint32_t (&c)[M],
+    const uint32_t (&SBC)[M], const uint32_t (&K)[M], const uint32_t (&DMC)[M], uint32_t Q,
+    const PencilArgs &pa,
+    const uint32_t (&inIx)[M], const uint32_t (&inIy)[M], const uint32_t (&inIz)[M],
+    const uint32_t (&inIxy)[M], const uint32_t (&inIyz)[M], const uint32_t (&inIxz)[M],
+    const uint32_t (&inM)[M], uint32_t (&nIx)[M], uint32_t (&oIy)[M], uint32_t (&oIz)[M],
+    uint32_t (&oIxy)[M], uint32_t (&oIyz)[M], uint32_t (&oIxz)[M], uint32_t (&oBest)[M]) {
+  const h2 DM = H(pa.h_dm), LAM = H(pa.v_lam), CP = H(pa.v_cP), DO = H(pa.v_dO);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const h2 eab = H(umin2(a[i] & b[i], Q)), eac = H(a[i] & c[i]), DMCi = H(DMC[i]);
+    const h2 sXY = hfma(eab, DM, H(inIxy[i]));  // src/PE_1cyc.v:159-161 (+mismatch folded)
+    const h2 sXZ = hfma(eac, DMCi, H(inIxz[i]));
+    const h2 sYZ = H(inIyz[i]) + H(SBC[i]);
+    h2 sM;                                       // src/PE_1cyc.v:162
+    if constexpr (SOP) sM = hfma(eab, DM, hfma(eac, DMCi, H(inM[i]))) + H(K[i]);
+    else sM = hfma(eab, H(K[i]), H(inM[i]));     // ne + 3 lam = 0
+    const h2 sX = H(inIx[i]), sY = H(inIy[i]), sZ = H(inIz[i]);
+    const h2 Gx = vmax3(sY, sZ, sYZ), Gy = vmax3(sX, sZ, sXZ), Gz = vmax3(sX, sY, sXY);
+    const h2 best = vmax3(Gx, Gy, hmax(sXY, sM));
+    const h2 b1 = best - DO;
+    const h2 pXY = hmax(Gz, b1), pYZ = hmax(Gx, b1), pXZ = hmax(Gy, b1);
+    const h2 qXY = pXY - CP, qYZ = pYZ - CP, qXZ = pXZ - CP;
+    oBest[i] = U(best);
+    oIxy[i] = U(pXY);
+    oIyz[i] = U(pYZ);
+    oIxz[i] = U(pXZ);
+    nIx[i] = U(vmax3(sX - LAM, qXY, qXZ));
+    oIy[i] = U(vmax3(sY - LAM, qXY, qYZ));
+    oIz[i] = U(vmax3(sZ - LAM, qYZ, qXZ));
+  }
+}
+
 // Shift a packed per-position value one position up the helix (k <- k-1).
 // With k = 64M*h + M*lane + i, register i >= 1 takes register i-1 of the same
 // lane (a rename, no instruction); register 0 takes register M-1 of lane-1
@@ -396,15 +450,13 @@ __device__ __forceinline__ void pos_split(int32_t k, int32_t &l, int32_t &i, int
   } while (0)
 
 // Host: packed constants of a parameter set (pencil_kernel.hip).
-PencilArgs make_args(const KParams &kp, bool f16);
+PencilArgs make_args(const KParams &kp, bool f16, bool vs);
 
-// Instantiated shapes: M = 1, 2 with 8 or 16 rows per workgroup; M = 4, 8
-// (LC up to 512 / 1024) with 8; each in f16 / int16 arithmetic and RTL / SOP s3.
-#define TSA_SHAPES(LAUNCH, M_, NW_, F16_, SOP_, ...)                                      \
-  ((M_) == 1 ? ((NW_) == 16 ? TSA_ARITH(LAUNCH, 1, 16, F16_, SOP_, __VA_ARGS__)            \
-                            : TSA_ARITH(LAUNCH, 1, 8, F16_, SOP_, __VA_ARGS__))            \
-   : (M_) == 2 ? ((NW_) == 16 ? TSA_ARITH(LAUNCH, 2, 16, F16_, SOP_, __VA_ARGS__)          \
-                              : TSA_ARITH(LAUNCH, 2, 8, F16_, SOP_, __VA_ARGS__))          \
+// Instantiated helix shapes: M = 1, 2, 4, 8 pairs per lane (LC up to 128 M),
+// 8 rows per workgroup; each in f16 / int16 arithmetic and RTL / SOP s3.
+#define TSA_SHAPES(LAUNCH, M_, F16_, SOP_, ...)                                            \
+  ((M_) == 1 ? TSA_ARITH(LAUNCH, 1, 8, F16_, SOP_, __VA_ARGS__)                            \
+   : (M_) == 2 ? TSA_ARITH(LAUNCH, 2, 8, F16_, SOP_, __VA_ARGS__)                          \
    : (M_) == 4 ? TSA_ARITH(LAUNCH, 4, 8, F16_, SOP_, __VA_ARGS__)                          \
                : TSA_ARITH(LAUNCH, 8, 8, F16_, SOP_, __VA_ARGS__))
 #define TSA_ARITH(LAUNCH, MM, NN, F16_, SOP_, ...)                                        \

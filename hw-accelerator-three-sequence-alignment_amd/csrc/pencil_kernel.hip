@@ -41,9 +41,10 @@
 namespace tsa {
 
 
-// waves (= DP rows) per lap: 16 (one 1024-thread WG per CU) or 8 (two WGs
-// per CU, so one computes while the other waits at its per-step barrier)
-constexpr int PENCIL_NW_DEFAULT = 8;
+// waves (= DP rows) per lap: 8, two workgroups per CU, so one computes while
+// the other waits at its barrier (16 rows in one 1024-thread workgroup measured
+// slower in round 1 and dropped)
+constexpr int PENCIL_NW = 8;
 constexpr int STORE_SLACK = 4;     // last wave keeps <= this many steps of stores in flight
 constexpr int MAX_LA = 4096, MAX_LB = 4096, MAX_LC = 1024;
 // LDS-DMA prefetch distance (steps) of wave 0: helix (ring) and lap (hand-off);
@@ -66,12 +67,7 @@ struct PencilGeom {
 // waves per CU the VGPR budget allows: 4 per SIMD up to M = 2, 2 beyond
 static int waves_per_cu(int M) { return M >= 4 ? 8 : 16; }
 
-// Helix rows per workgroup: 8 (two WGs per CU) or 16; M >= 4 always 8.
-static int helix_nw(int M) {
-  if (M >= 4) return 8;
-  if (const char *e = getenv("TSA_PENCIL_NW")) return atoi(e) == 16 ? 16 : 8;  // tuning knob
-  return PENCIL_NW_DEFAULT;
-}
+static int helix_nw(int) { return PENCIL_NW; }
 // TWO: for LC <= 64 a wave's two 16-bit halves hold two different triples at
 // the same 64 positions (a lane = one z of both), instead of positions k and
 // k+64 of one triple -- no idle half, and the lap period shrinks to max(LA, 64).
@@ -108,6 +104,7 @@ static bool pencil_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc) {
 }
 
 static bool use_f16(const KParams &kp, const Range &r);
+static bool use_vs(const KParams &kp, const Range &r, int32_t max_la, int32_t max_lb, int32_t max_lc);
 
 // Estimated latency (us) of the helix kernel for a batch: dispatch waves x
 // steps per triple x step time. Measured: a fully loaded chip (two 8-wave
@@ -198,8 +195,11 @@ bool pencil_shape_supported(int32_t max_la, int32_t max_lb, int32_t max_lc) {
 //        sA2 [P+ZT] u32            A codes for positions k and k+64 of one pair
 //        sB  [LB] u32              B code, both halves
 //        fin [M][64] u32           best of the final step (wave w_f)
-// F16 selects the exact-f16 arithmetic above, else the int16 form.
-template <int M, int NW, bool F16, bool SOP, bool TWO>
+// F16 selects the exact-f16 arithmetic above, else the int16 form; VS the
+// V-space f16 cell (cell_messages_vs): every value shifted by lam*(x+y+z), the
+// zero faces injected as lam*q (x = 1: H(t), H(t-1); z = 0: H(t+1), H(t+2);
+// y = 0: the ring's face records), the score shifted back at the end.
+template <int M, int NW, bool F16, bool SOP, bool TWO, bool VS>
 __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restrict__ seqs,
                                                          const int64_t *__restrict__ offs,
                                                          int32_t n, int32_t P, int32_t R,
@@ -223,6 +223,12 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   static_assert(!TWO || M == 1, "two triples per wave: 64 positions, M = 1");
+  static_assert(!VS || (F16 && M <= 2), "V-space: the f16 helix with the four-step loop");
+  // f16 bits of an integer (|v| <= 2048: exact), in both halves
+  auto h_bits = [](int32_t v) -> uint32_t {
+    const _Float16 h = (_Float16)(float)v;
+    return (uint32_t)__builtin_bit_cast(uint16_t, h) * 0x00010001u;
+  };
   // TWO: the halves are two triples at the same position, so lane 0 takes its
   // whole word from the z = 0 face (no half crosses from lane 63)
   const uint32_t sel = lane == 0 ? (TWO ? 0x03020100u : 0x05040302u) : 0x07060504u;
@@ -269,10 +275,22 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       else
         sB[i] = (SYM0 << tsa_sym(seqs, o1 + i, pa.packed)) * 0x00010001u;
     }
+    // ring rows of wave 0's lap 0 -> ring row (t - lag) mod R at step t
+    const int32_t lag = P - HSK * (NW - 1);
     {
       const uint4 face = make_uint4(pa.f_single, pa.f_pair, pa.f_pair, 0u);
       const int64_t n16 = (int64_t)R * M * 64;
-      for (int64_t i = threadIdx.x; i < n16; i += 64 * NW) ((uint4 *)ring)[i] = face;
+      for (int64_t i = threadIdx.x; i < n16; i += 64 * NW) {
+        if constexpr (VS) {
+          // row 0's face cells as wave 0 meets them at step tr: x + z = tr + 2 for
+          // every position ({Iy, Ixy, Iyz, best} = lam q - lam, lam q x 3)
+          const int32_t tr = (int32_t)((i / (M * 64) + lag) % R);
+          const uint32_t f1 = h_bits(pa.lam * (tr + 1)), f2 = h_bits(pa.lam * (tr + 2));
+          ((uint4 *)ring)[i] = make_uint4(f1, f2, f2, f2);
+        } else {
+          ((uint4 *)ring)[i] = face;
+        }
+      }
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
@@ -335,8 +353,21 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     const int32_t t_f1 = ((lb1 - 1) / NW) * P + (la1 - 1) + HSK * w_f1 + k_f1;
     const int32_t T = (TWO ? max(t_f, t_f1) : t_f) + 1;
 
+    // VS: Hr[s & 3] = H(s) = lam * (y + xpos0) at step s (y: position 0's row,
+    // 1-based) -- the x = 0 face at the x = 1 position and, one and two steps
+    // ahead, the z = 0 face of position 0; one v_pk_add per step, reset at a wrap
+    uint32_t Hr[4] = {0u, 0u, 0u, 0u};
+    auto h_at = [&](int32_t s) -> uint32_t {
+      const int32_t u = s - HSK * w;
+      const int32_t lp = u >= 0 ? u / P : -((P - 1 - u) / P);
+      return h_bits(pa.lam * (lp * NW + w + 1 + (u - lp * P)));
+    };
+    if constexpr (VS) {
+      Hr[3] = h_at(-1);
+      Hr[0] = h_at(0);
+      Hr[1] = h_at(1);
+    }
     // wave 0: prime the LDS-DMA pipeline (ring row of step s = s - P + NW - 1)
-    const int32_t lag = P - HSK * (NW - 1);
     if (w == 0) {
 #pragma unroll 1
       for (int s = 0; s < PD; ++s) {
@@ -419,10 +450,17 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll
         for (int i = 0; i < M; ++i) {
           if (ISC >= 0 ? i == ISC : i == is) {
-            inIx[i] = vbfi(m1, fsv, inIx[i]);
-            inIxy[i] = vbfi(m1, fpv, inIxy[i]);
-            inIxz[i] = vbfi(m1, fpv, inIxz[i]);
-            inM[i] = vbfi(m1, zero, inM[i]);
+            if constexpr (VS) {  // faces (0,y,z), (0,y-1,z), (0,y,z-1): lam(y+z-1); (0,y-1,z-1): one lam less
+              inIx[i] = vbfi(m1, Hr[PQ & 3], inIx[i]);
+              inIxy[i] = vbfi(m1, Hr[PQ & 3], inIxy[i]);
+              inIxz[i] = vbfi(m1, Hr[PQ & 3], inIxz[i]);
+              inM[i] = vbfi(m1, Hr[(PQ + 3) & 3], inM[i]);
+            } else {
+              inIx[i] = vbfi(m1, fsv, inIx[i]);
+              inIxy[i] = vbfi(m1, fpv, inIxy[i]);
+              inIxz[i] = vbfi(m1, fpv, inIxz[i]);
+              inM[i] = vbfi(m1, zero, inM[i]);
+            }
             b[i] = vbfi(m1, binj, b[i]);
             if constexpr (F16) {  // the new row's per-row terms
 #if TSA_ROW_NEXT
@@ -449,7 +487,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       // of a SIMD finish each step first and idle at the barrier (+3-4 %).
       if constexpr (TSA_SETPRIO) __builtin_amdgcn_s_setprio(0);
       if constexpr (TSA_SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);  // keep the arithmetic between the two
-      if constexpr (F16)
+      if constexpr (VS)
+        cell_messages_vs<M, SOP>(a, b, c, SBC, K, DMC, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx,
+                                 oIy, oIz, oIxy, oIyz, oIxz, oBest);
+      else if constexpr (F16)
         cell_messages_f16<M, SOP>(a, b, c, SBC, K, DMC, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx,
                              oIy, oIz, oIxy, oIyz, oIxz, oBest);
       else
@@ -463,6 +504,11 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       if constexpr (TWO) {  // two final cells, possibly at different steps
         if (t == t_f && w == w_f) fin[lane] = oBest[0];
         if (t == t_f1 && w == w_f1) fin[64 + lane] = oBest[0];
+      } else if constexpr (VS) {  // the four-step loop runs past T: the final step is tested
+        if (t == T - 1 && w == w_f) {
+#pragma unroll
+          for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
+        }
       } else if constexpr (FIN) {
         if (w == w_f) {
 #pragma unroll
@@ -481,14 +527,18 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         // y = 0 face: wave 0 reads this row as "row y0-1" during its lap 0.
         if (t < ZT + HSK * NW) {
           const int32_t lim = t - HSK * w;  // position k started iff k <= lim
+          // VS: wave 0 meets this row at step t + lag, where x + z = t + lag + 2
+          const uint32_t fy = VS ? h_bits(pa.lam * (t + lag + 1)) : pa.f_single;
+          const uint32_t fp = VS ? h_bits(pa.lam * (t + lag + 2)) : pa.f_pair;
+          const uint32_t fb = VS ? fp : 0u;
 #pragma unroll
           for (int i = 0; i < M; ++i) {
             const uint32_t m = ((M * lane + i > lim) ? 0x0000FFFFu : 0u) |
                                (((TWO ? 0 : 64 * M) + M * lane + i > lim) ? 0xFFFF0000u : 0u);
-            oIy[i] = bfi(m, pa.f_single, oIy[i]);
-            oIxy[i] = bfi(m, pa.f_pair, oIxy[i]);
-            oIyz[i] = bfi(m, pa.f_pair, oIyz[i]);
-            oBest[i] = bfi(m, 0u, oBest[i]);
+            oIy[i] = bfi(m, fy, oIy[i]);
+            oIxy[i] = bfi(m, fp, oIxy[i]);
+            oIyz[i] = bfi(m, fp, oIyz[i]);
+            oBest[i] = bfi(m, fb, oBest[i]);
           }
         }
         uint4 *dst = (uint4 *)__builtin_assume_aligned(
@@ -505,28 +555,49 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       uint32_t rz[M], rw[M];
 #pragma unroll
       for (int i = 0; i < M; ++i) { rz[i] = rec[i].z; rw[i] = rec[i].w; }
-      zshift<M>(shIxz[PH], oIxz, sel, pa.f_pair);  // z = 0 face for position 0
-      zshift<M>(shIz, oIz, sel, pa.f_single);
-      zshift<M>(svIyz, rz, sel, pa.f_pair);
-      zshift<M>(svM[PH], rw, sel, 0u);
       // position 0 advances to u0 + 1
+      auto advance = [&]() {
 #if TSA_HM_TRACK
-      if (__builtin_expect(++xpos0 == next_ev, 0)) {
-        if (xpos0 == P) {
+        if (__builtin_expect(++xpos0 == next_ev, 0)) {
+          if (xpos0 == P) {
+            xpos0 = 0;
+            binj = b_of_lap(++lap0);
+            row_terms();
+            if constexpr (VS) {  // a new row at position 0: H(t .. t+2) restart
+              const int32_t y = lap0 * NW + w + 1;
+              Hr[PQ & 3] = h_bits(pa.lam * (y - 1));
+              Hr[(PQ + 1) & 3] = h_bits(pa.lam * y);
+              Hr[(PQ + 2) & 3] = h_bits(pa.lam * (y + 1));
+            }
+          }
+          hmCur = hm_of(xpos0);
+          next_ev = ev_of(xpos0);
+        }
+#else
+        static_assert(!VS, "V-space tracks the lap wrap with the half-mask events");
+        if (++xpos0 == P) {
           xpos0 = 0;
           binj = b_of_lap(++lap0);
           row_terms();
         }
-        hmCur = hm_of(xpos0);
-        next_ev = ev_of(xpos0);
-      }
-#else
-      if (++xpos0 == P) {
-        xpos0 = 0;
-        binj = b_of_lap(++lap0);
-        row_terms();
-      }
 #endif
+      };
+      if constexpr (VS) {
+        Hr[(PQ + 2) & 3] = U(H(Hr[(PQ + 1) & 3]) + H(pa.v_lam));
+        advance();
+        // z = 0 faces of position 0: (x, y, 0) and (x, y-1, 0) at step t+1,
+        // (x-1, y, 0) and (x-1, y-1, 0) at step t+2
+        zshift<M>(shIxz[PH], oIxz, sel, Hr[(PQ + 2) & 3]);
+        zshift<M>(shIz, oIz, sel, Hr[(PQ + 1) & 3]);
+        zshift<M>(svIyz, rz, sel, Hr[(PQ + 1) & 3]);
+        zshift<M>(svM[PH], rw, sel, Hr[(PQ + 1) & 3]);
+      } else {
+        zshift<M>(shIxz[PH], oIxz, sel, pa.f_pair);  // z = 0 face for position 0
+        zshift<M>(shIz, oIz, sel, pa.f_single);
+        zshift<M>(svIyz, rz, sel, pa.f_pair);
+        zshift<M>(svM[PH], rw, sel, 0u);
+        advance();
+      }
       if constexpr (TSA_A_PREFETCH) load_a<M>(a_lane + 4u * (uint32_t)xpos0, a_nx);
 
       // ---- wave 0: fetch the record of step t + PD into the slot just consumed
@@ -563,6 +634,16 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       constexpr std::integral_constant<int, 3> Q3{};
       constexpr std::false_type mid{};
       constexpr std::true_type last{};
+      if constexpr (VS) {  // whole groups of four steps (H's phase is t & 3), the final cell tested
+#pragma unroll 1
+        for (; t < T; t += 4) {
+          TSA_INLINE_IF_WIDE(step(Q0, role, t, mid));
+          TSA_INLINE_IF_WIDE(step(Q1, role, t + 1, mid));
+          TSA_INLINE_IF_WIDE(step(Q2, role, t + 2, mid));
+          TSA_INLINE_IF_WIDE(step(Q3, role, t + 3, mid));
+        }
+        return;
+      }
 #if TSA_UNROLL4
 #pragma unroll 1
       for (; (M <= 2 || HSK == 2) && t + 3 < T1; t += 4) {
@@ -597,14 +678,16 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       auto decode = [&](uint16_t hb) -> int32_t {
         return F16 ? (int32_t)(float)__builtin_bit_cast(_Float16, hb) : (int32_t)(int16_t)hb;
       };
+      // VS: the final cell's value sits lam (la + lb + lc) above its score
+      const int32_t sh0 = VS ? pa.lam * (la + lb + lc) : 0, sh1 = VS ? pa.lam * (la1 + lb1 + lc1) : 0;
       if constexpr (TWO) {
-        scores[tri] = decode((uint16_t)(fin[k_f] & 0xFFFF));
-        if (has1) scores[tri + 1] = decode((uint16_t)(fin[64 + k_f1] >> 16));
+        scores[tri] = decode((uint16_t)(fin[k_f] & 0xFFFF)) - sh0;
+        if (has1) scores[tri + 1] = decode((uint16_t)(fin[64 + k_f1] >> 16)) - sh1;
       } else {
         int32_t l_f, i_f, h_f;
         pos_split<M>(k_f, l_f, i_f, h_f);
         const uint32_t v = fin[i_f * 64 + l_f];
-        scores[tri] = decode((uint16_t)(h_f ? (v >> 16) : (v & 0xFFFF)));
+        scores[tri] = decode((uint16_t)(h_f ? (v >> 16) : (v & 0xFFFF))) - sh0;
       }
     }
     __syncthreads();
@@ -619,7 +702,7 @@ static uint32_t pkh(double v) {  // both halves = f16(v); v exactly representabl
   return (uint32_t)bits * 0x00010001u;
 }
 
-PencilArgs make_args(const KParams &kp, bool f16) {
+PencilArgs make_args(const KParams &kp, bool f16, bool vs) {
   const int32_t GE = kp.pen[SIXY][SIX], GO = kp.pen[SIXY][SM];  // Ixy row: Ix = GE, M = GO
   int32_t fs = -kp.pen[SIX][0], fp = -kp.pen[SIXY][0];
   for (int s = 0; s < 7; ++s) {
@@ -662,6 +745,17 @@ PencilArgs make_args(const KParams &kp, bool f16) {
   const uint32_t k1 = a.sop ? pkh(3.0 * mm + dm) : pkh((d0 + d1) * 8192.0);
   a.h_k0 = k0;                // K = k0 + e01 * (k1 - k0), per 16-bit half
   a.h_kd = (((k1 & 0xFFFF) - (k0 & 0xFFFF)) & 0xFFFF) * 0x00010001u;
+  if (vs) {  // cell_messages_vs: lam = GE = -mismatch; SOP's K takes the 3 lam of M
+    a.lam = GE;
+    a.v_lam = pkh(GE);
+    a.v_cP = pkh(GO + mm + GE);
+    a.v_dO = pkh(GO - GE);
+    if (a.sop) {
+      const uint32_t k0v = pkh(3.0 * mm + 3.0 * GE), k1v = pkh(3.0 * mm + dm + 3.0 * GE);
+      a.h_k0 = k0v;
+      a.h_kd = (((k1v & 0xFFFF) - (k0v & 0xFFFF)) & 0xFFFF) * 0x00010001u;
+    }
+  }
   return a;
 }
 
@@ -677,8 +771,10 @@ int64_t pencil_slack(int32_t match, int32_t mismatch, int32_t gap_open, int32_t 
 
 // Exact-f16 arithmetic applies when every value and intermediate is an integer
 // in [-2048, 2048] (value bound +- pencil_slack) and the scaled deltas fit f16.
+// TSA_PENCIL_ARITH (A/B and test knob): "i16" forces the int16 form, "f16"
+// the f16 form without V-space.
 static bool use_f16(const KParams &kp, const Range &r) {
-  if (const char *e = getenv("TSA_PENCIL_ARITH"))  // tuning / test knob
+  if (const char *e = getenv("TSA_PENCIL_ARITH"))
     if (!strcmp(e, "i16")) return false;
   auto small = [](int64_t v) { return v >= -7 && v <= 7; };
   auto fits = [](int64_t v) { return v >= -2048 && v <= 2048; };
@@ -690,15 +786,31 @@ static bool use_f16(const KParams &kp, const Range &r) {
          fits(3LL * kp.mismatch);
 }
 
+// The V-space f16 helix (cell_messages_vs) applies when lam = GE = -MISMATCH
+// (the RTL constants: 1), the helix runs M <= 2, and the shifted values stay
+// exact f16 integers: bound + lam (LA + LB + LC) + slack <= 2048.
+static bool use_vs(const KParams &kp, const Range &r, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  if (const char *e = getenv("TSA_PENCIL_ARITH"))
+    if (!strcmp(e, "i16") || !strcmp(e, "f16")) return false;
+  const int32_t GE = kp.pen[SIXY][SIX], GO = kp.pen[SIXY][SM];
+  if (!use_f16(kp, r) || pencil_pairs(max_lc) > 2 || GE < 1 || GE != -kp.mismatch || GO < GE) return false;
+  const int64_t slack = pencil_slack(kp.match, kp.mismatch, GO, GE);
+  const int64_t hi = r.hi + (int64_t)GE * ((int64_t)max_la + max_lb + max_lc) + slack;
+  return r.lo - slack >= -2048 && hi <= 2048 && (int64_t)GO + GE + kp.mismatch <= 2048;
+}
+
 template <int M, int NW, bool F16, bool SOP>
 static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                     int32_t max_lb, const PencilGeom &g, int32_t *d_scores, void *d_ws,
                     const PencilArgs &pa, hipStream_t stream) {
+  constexpr bool VSOK = F16 && M <= 2;  // V-space instantiations
+  const bool vs = VSOK && pa.lam != 0;
   const int32_t lds_a = 4 * (g.P + 128 * M), lds_b = 4 * ((max_lb + 3) & ~3);
   const size_t lds = helix_lds(M, NW, g.P, max_lb);
   // TWO (two triples per workgroup) exactly when pencil_geom sized P for it
   const bool two = M == 1 && g.two;
-  auto kfn = two ? pencil_kernel<M, NW, F16, SOP, M == 1> : pencil_kernel<M, NW, F16, SOP, false>;
+  auto kfn = vs ? (two ? pencil_kernel<M, NW, F16, SOP, M == 1, VSOK> : pencil_kernel<M, NW, F16, SOP, false, VSOK>)
+                : (two ? pencil_kernel<M, NW, F16, SOP, M == 1, false> : pencil_kernel<M, NW, F16, SOP, false, false>);
   if (lds > LDS_MAX) return TSA_EINVAL;
   if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)lds) != hipSuccess)
@@ -723,6 +835,7 @@ void pencil_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, 
     return;
   }
   const PencilGeom g = pencil_geom(max_la, max_lc);
+  if (use_vs(kp, bound, max_la, max_lb, max_lc)) arith = "f16v";  // the helix's V-space cell
   snprintf(buf, len, "pencil helix %s %s M=%d NW=%d P=%d%s", arith, s3, g.M, helix_nw(g.M), g.P,
            g.two ? " two" : "");
 }
@@ -736,18 +849,19 @@ int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t
   if (n <= 0) return TSA_OK;
   if (!pencil_shape_ok(max_la, max_lb, max_lc)) return TSA_EINVAL;
   const bool f16 = chk ? false : use_f16(kp, bound);  // the checked kernel runs int16
-  const PencilArgs pa = make_args(kp, f16);
-  const bool sop = pa.sop != 0;
+  const bool sop = kp.s3_mode == TSA_S3_SOP;
   const LapGeom lg = lap_choice(n, max_la, max_lb, max_lc, lap, f16, sop, chk != nullptr);
   if (lg.ok) {
     if (ws_bytes < lap_workspace_bytes(lg)) return TSA_ENOMEM;
-    return lap_launch(lg, f16, sop, d_seqs, d_offsets, n, d_scores, d_ws, pa, stream, d_err, chk);
+    return lap_launch(lg, f16, sop, d_seqs, d_offsets, n, d_scores, d_ws, make_args(kp, f16, false), stream,
+                      d_err, chk);
   }
+  const PencilArgs pa = make_args(kp, f16, !chk && use_vs(kp, bound, max_la, max_lb, max_lc));
   if (chk) return TSA_ERANGE;  // no lap schedule for this batch
   const PencilGeom g = pencil_geom(max_la, max_lc);
   const int32_t grid = n < 65535 ? n : 65535;
   if (ws_bytes < (size_t)grid * (size_t)g.ring_bytes_per_triple) return TSA_ENOMEM;
-  return TSA_SHAPES(launch_m, g.M, helix_nw(g.M), f16, sop, d_seqs, d_offsets, n, max_lb, g,
+  return TSA_SHAPES(launch_m, g.M, f16, sop, d_seqs, d_offsets, n, max_lb, g,
                     d_scores, d_ws, pa, stream);
 }
 
@@ -774,7 +888,7 @@ LapGeom pencil_split_geom(int32_t la, int32_t lb, int32_t lc, const KParams &kp,
 int pencil_launch_split(const LapGeom &g, const KParams &kp, const Range &bound, const LapPart *parts,
                         int np, int32_t *d_score, uint32_t *d_err) {
   const bool f16 = use_f16(kp, bound);
-  const PencilArgs pa = make_args(kp, f16);
+  const PencilArgs pa = make_args(kp, f16, false);
   return lap_launch_split(g, f16, pa.sop != 0, pa, parts, np, d_score, d_err);
 }
 #undef TSA_SHAPES

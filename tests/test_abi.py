@@ -84,7 +84,11 @@ def test_describe_plan(tsa):
     # streaming lap window of the sync path, and parameter sets the pencil
     # arithmetic does not cover
     p = tsa.TsaParams.default()
-    assert tsa.describe_plan(512, 256, 256, 256, p).startswith("pencil helix f16 rtl M=2 NW=8")
+    assert tsa.describe_plan(512, 256, 256, 256, p).startswith("pencil helix f16v rtl M=2 NW=8")
+    # V-space needs lam = GE = -MISMATCH and the shifted values inside exact f16
+    assert tsa.describe_plan(512, 256, 256, 256, tsa.TsaParams.default(gap_extend=2, gap_open=3)
+                             ).startswith("pencil helix f16 rtl")
+    assert tsa.describe_plan(512, 400, 400, 400, p).startswith("pencil helix f16 rtl M=4")
     assert tsa.describe_plan(1, 256, 256, 256, p).startswith("pencil lap f16 rtl M=1")
     # a few cubes: the lap kernel; many: the helix; the synchronous path may
     # stream a lap grid beyond the resident slots (waves > 1), the async one not
