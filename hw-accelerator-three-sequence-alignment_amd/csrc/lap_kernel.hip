@@ -69,9 +69,6 @@ namespace tsa {
 #ifndef TSA_LAP_PD4
 #define TSA_LAP_PD4 3
 #endif
-#ifndef TSA_LAP_DELAY  // loader start lag behind the producers (steps), see the loader
-#define TSA_LAP_DELAY 0
-#endif
 __host__ __device__ constexpr int lap_pd(int M) {
   return M == 1 ? TSA_LAP_PD1 : M == 2 ? TSA_LAP_PD2 : TSA_LAP_PD4;
 }
@@ -99,9 +96,10 @@ static size_t lap_lds_bytes(int M, int NW, int32_t max_la) {
          4 * (((size_t)max_la + 2 * ZT + 4 * NW + 8 + 3) & ~(size_t)3);
 }
 
-// Trace slots per block (TSA_LAP_TRACE): 8, plus with TSA_LAP_PROF (a
-// diagnostic build) 4 shader-clock accumulators per compute wave.
-#if defined(TSA_LAP_PROF)
+// Trace slots per block (TSA_LAP_TRACE): 8, plus with TSA_DIAG (the
+// diagnostic build, scripts/build_variant.sh) 4 shader-clock accumulators per
+// compute wave.
+#if defined(TSA_DIAG)
 constexpr int LAP_TRACE_SLOTS = 8 + 4 * 8;
 #else
 constexpr int LAP_TRACE_SLOTS = 8;
@@ -148,9 +146,6 @@ __device__ __forceinline__ int32_t lds_word(const int32_t *p) {
 // from moving LDS accesses across it.
 __device__ __forceinline__ void lds_publish(int32_t *pw_wave, int32_t v, int lane) {
   asm volatile("" ::: "memory");
-#if defined(TSA_LAP_LDS_FENCE)  // A/B knob: drain this wave's LDS writes first
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
   *(volatile __attribute__((address_space(3))) int32_t *)(__attribute__((address_space(3))) void *)(
       pw_wave + lane) = v;
   asm volatile("" ::: "memory");
@@ -554,25 +549,6 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       }
     }
     __syncthreads();  // (matches the compute waves' prologue barrier)
-#if TSA_LAP_DELAY > 0
-    // Start the prefetch window TSA_LAP_DELAY steps behind the producers'
-    // frontier: wait until the records that far ahead are stored, so a window
-    // deeper than the frontier allows (LPD) fetches stored records instead of
-    // stale ones -- the loader then delivers LPD records per round trip.
-    {
-      Fetch f;
-      const int32_t dy = min(TSA_LAP_DELAY, T_above - YOFF - 1);
-      if (yin && dy > 0) {
-        fetch_y(dy, f);
-        if (!y_ok(dy, f)) settle_y(dy, f);
-      }
-      const int32_t dz = min(ZT + ZA + TSA_LAP_DELAY, T_left - 1);
-      if (zin && dz >= ZT + ZA) {
-        fetch_z(dz, f);
-        if (!z_ok(dz, f)) settle_z(dz, f);
-      }
-    }
-#endif
     Fetch fq[LPD];
 #pragma unroll
     for (int j = 0; j < LPD; ++j) fetch(j, fq[j]);
@@ -686,7 +662,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
     // wave; z: the tile to the right, every wave), LDS-DMA'd by the loader
     int32_t seen_in = 0, seen_out = 0, seen_y = 0, seen_z = 0;
     uint32_t n_bp = 0;
-#if defined(TSA_LAP_PROF)  // shader cycles: reads + pre-cell, check, post + stores, step gap
+#if defined(TSA_DIAG)  // shader cycles: reads + pre-cell, check, post + stores, step gap
     uint64_t prof[4] = {0, 0, 0, 0}, prof_last = 0;
 #endif
     constexpr int LM = M == 1 ? 0 : M == 2 ? 1 : M == 4 ? 2 : 3;  // log2 M
@@ -728,7 +704,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       // cached value covers step t), then its record. LDS executes a wave's DS
       // instructions in order, so a word read that covers t proves the record
       // read behind it current; the check waits until the pre-cell is done.
-#if defined(TSA_LAP_PROF)
+#if defined(TSA_DIAG)
       const uint64_t pt0 = __builtin_amdgcn_s_memtime();
 #endif
       const int32_t need = ROLE == 0 ? t + 1 : t;
@@ -803,7 +779,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       for (int i = 0; i < M; ++i)
         asm volatile("" : "+v"(pre.W[i]), "+v"(pre.N1[i]), "+v"(pre.N2[i]), "+v"(pre.N3[i]),
                      "+v"(pre.N4[i]), "+v"(pre.N5[i]), "+v"(pre.N6[i]));
-#if defined(TSA_LAP_PROF)
+#if defined(TSA_DIAG)
       const uint64_t pt1 = __builtin_amdgcn_s_memtime();
 #endif
       // ---- the input record is current? (slow path: poll, then read it again)
@@ -832,21 +808,13 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
           Rb[i] = perm(pBest[i], rv[i].z, 0x05040302u);
         }
       }
-#if defined(TSA_LAP_PROF)
+#if defined(TSA_DIAG)
       asm volatile("" :: "v"(Ry[0]));
       const uint64_t pt2 = __builtin_amdgcn_s_memtime();
 #endif
       uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
-#if defined(TSA_EXP_NOCELL)  // timing-only experiment: no cell arithmetic after the record
-#pragma unroll
-      for (int i = 0; i < M; ++i) {
-        nIx[i] = pre.N1[i]; oIy[i] = Ry[i]; oIz[i] = pre.N3[i]; oIxy[i] = pre.N4[i];
-        oIyz[i] = pre.N5[i]; oIxz[i] = pre.N6[i]; oBest[i] = pre.W[i];
-      }
-#else
       if constexpr (F16) lap_post_f16<M>(pa, Ry, pre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
       else lap_post_i16<M>(pv, Ry, pre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
-#endif
       if constexpr (CHK) {
 #pragma unroll
         for (int i = 0; i < M; ++i) {
@@ -903,7 +871,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
         }
       }
       lds_publish(pw + 64 * w, t + 1, lane);
-#if defined(TSA_LAP_PROF)
+#if defined(TSA_DIAG)
       const uint64_t pt3 = __builtin_amdgcn_s_memtime();
       prof[0] += pt1 - pt0;
       prof[1] += pt2 - pt1;
@@ -946,13 +914,9 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       }
     };
     static_assert(NW >= 2, "wave 0 and the last wave are distinct roles");
-#if defined(TSA_EXP_ALLMID)  // timing-only experiment: every wave runs the middle role
-    LAP_INLINE(run(std::integral_constant<int, 1>{}));
-#else
     if (w == 0) LAP_INLINE(run(std::integral_constant<int, 0>{}));
     else if (w == NW - 1) LAP_INLINE(run(std::integral_constant<int, 2>{}));
     else LAP_INLINE(run(std::integral_constant<int, 1>{}));
-#endif
     if (trace != nullptr) {
       const unsigned long long clk1 = __builtin_amdgcn_s_memtime();
       stamp(2, now());
@@ -982,7 +946,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
         atomicMin(mon + ntri + tri, mn);
       }
     }
-#if defined(TSA_LAP_PROF)
+#if defined(TSA_DIAG)
     if (trace != nullptr && lane == 0 && w < 8)
       for (int k = 0; k < 4; ++k) trace[(int64_t)b * LAP_TRACE_SLOTS + 8 + 4 * w + k] = prof[k];
 #endif
@@ -1069,8 +1033,9 @@ static double lap_step_us(int M, int NW, int64_t wg_per_cu) {
 
 LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW,
                  bool full_rings, bool f16, bool sop) {
-  // A/B knob: full-length rings (no back-pressure) on every lap launch
+#if defined(TSA_DIAG)  // A/B knob: full-length rings (no back-pressure) on every lap launch
   if (const char *e = getenv("TSA_LAP_FULL_RINGS")) full_rings = full_rings || atoi(e) != 0;
+#endif
   LapGeom g{};
   g.M = M;
   g.NW = NW;
@@ -1087,11 +1052,12 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   // made producers wait (1024^3: 1235 back-pressure waits, 3.30 ms; 240 slots:
   // 34 waits, 3.06 ms, 580 MB). A/B knob TSA_LAP_RING_SLACK.
   int slack = std::max(max_la, std::max(max_lb, max_lc)) > 512 ? 240 : 48;
+#if defined(TSA_DIAG)
   if (const char *e = getenv("TSA_LAP_RING_SLACK")) slack = std::max(16, atoi(e));
+#endif
   g.YR = full_rings ? pow2(T) : pow2(YOFF + LPD + slack);
   g.ZR = full_rings ? pow2(T) : pow2(ZT + LPD + slack);
   g.lds = lap_lds_bytes(M, NW, max_la);
-  if (const char *e = getenv("TSA_LAP_LDS_EXTRA")) g.lds += (size_t)atoi(e);  // diagnostic knob
   const int64_t wgs = (int64_t)n * g.G * g.GZ;
   g.blocks = (int64_t)g.G * g.CH * 8;
   // progress words, the error word (+63 spare), the checked kernel's monitor (2 n)
@@ -1109,9 +1075,13 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   g.waves = per_cu > 0 ? std::max<int64_t>((wg_per_xcd + slots_xcd - 1) / slots_xcd,
                                            (wgs + (int64_t)cus * per_cu - 1) / ((int64_t)cus * per_cu))
                        : 0;
-  // one workgroup is the helix's job; TSA_LAP_SINGLE=1 allows it (diagnostics:
-  // the step time with no hand-off)
+  // one workgroup is the helix's job; a TSA_DIAG build allows it with
+  // TSA_LAP_SINGLE=1 (the step time with no hand-off)
+#if defined(TSA_DIAG)
   const bool single = getenv("TSA_LAP_SINGLE") && atoi(getenv("TSA_LAP_SINGLE")) != 0;
+#else
+  const bool single = false;
+#endif
   g.ok = per_cu > 0 && (g.G >= 2 || g.GZ >= 2 || single);
   // estimated latency (us): the chain to the final workgroup -- each lap adds
   // YOFF + LPD + ~3 steps, each tile ZT + LPD + ~2 -- plus its own steps;
@@ -1185,7 +1155,7 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
     (void)hipFree(trace);
     if (FILE *fp = fopen(tpath, "w")) {
       fprintf(fp, "block,tri,lap,tile,start,loop_begin,loop_end,xcc,stalls,w0_waits,loop_clk,bp_waits");
-      for (int k = 8; k < LAP_TRACE_SLOTS; ++k)  // TSA_LAP_PROF: wave (k-8)/4, phase (k-8)%4
+      for (int k = 8; k < LAP_TRACE_SLOTS; ++k)  // TSA_DIAG: wave (k-8)/4, phase (k-8)%4
         fprintf(fp, ",prof%d_%d", (k - 8) / 4, (k - 8) % 4);
       fprintf(fp, "\n");
       for (int64_t b = 0; b < g.blocks; ++b) {

@@ -422,11 +422,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         inIx[i] = oIx[i];
-#ifdef TSA_EXP_NOREC  // timing experiment only: wrong results
-        inIy[i] = oIx[i] ^ 1u;
-#else
         inIy[i] = rec[i].x;
-#endif
         inIz[i] = shIz[i];
         inIxy[i] = svIxy[i];
         inIyz[i] = svIyz[i];
@@ -612,12 +608,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         if (++st_row == R) st_row = 0;
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(M * STORE_SLACK) : "memory");
       }
-#ifdef TSA_EXP_NOBAR  // timing experiment only: wrong results
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
       // skew 2: a wave reads records two steps old, so one barrier per pair of steps
       if constexpr (HSK == 1 || PH == 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
     };
 
     // the last step is peeled off (it records the final cell), so the loop

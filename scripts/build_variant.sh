@@ -1,20 +1,23 @@
 #!/bin/bash
-# Build a variant of the package into scratch/<name>/ (same sources, extra -D
-# flags) for same-box A/B timing: TSA_PKG_DIR=scratch/<name> selects it.
+# Build a variant of the package into variants/<name>/ (same sources, extra -D
+# flags) for same-box A/B timing: TSA_PKG_DIR=variants/<name> selects it.
+# The diagnostic knobs (TSA_LAP_SINGLE, TSA_LAP_RING_SLACK, TSA_LAP_FULL_RINGS,
+# per-phase cycle counters) exist only in a -DTSA_DIAG build:
+#   scripts/build_variant.sh diag "-DTSA_DIAG"
 #   scripts/build_variant.sh nopf "-DTSA_A_PREFETCH=0"
 set -e
 cd "$(dirname "$0")/.."
 NAME=$1; DEFS=$2
 PKG=hw-accelerator-three-sequence-alignment_amd
 SRC=${SRC:-$PKG}  # source tree (e.g. a git archive of an older commit)
-OUT=scratch/$NAME
+OUT=variants/$NAME
 rm -rf "$OUT"; mkdir -p "$OUT/lib" "$OUT/build"
 cp $PKG/*.py "$OUT/"
 objs=()
 for f in $SRC/csrc/*.hip; do
   o="$OUT/build/$(basename "${f%.hip}").o"
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function \
-    -DTSA_GIT_DESCRIBE="\"variant-$NAME\"" $DEFS -c "$f" -o "$o" &
+    -DTSA_SRC_HASH="\"variant-$NAME\"" $DEFS -c "$f" -o "$o" &
   objs+=("$o")
 done
 wait

@@ -4,6 +4,7 @@
 set -o pipefail
 R="$GRAFT_REPO_ROOT"; TAG=${TAG:-lapsq}
 cd /tmp && export TMPDIR=/tmp
+export TSA_PKG_DIR=${TSA_PKG_DIR:-$GRAFT_REPO_ROOT/variants/diag}  # TSA_LAP_SINGLE needs the -DTSA_DIAG build
 OUT="$R/gpurun_out/pmc_${TAG}"; mkdir -p "$OUT"
 S=${SPECS:-"64x8x64:TSA_LAP_M=1,TSA_LAP_NW=4,TSA_LAP_SINGLE=1"}
 i=0

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Lap diagnostics (tools/lap_trace.py) for the in-tree package and each
-# scratch/<name> variant in $LIBS (scripts/build_variant.sh; timing-only
+# variants/<name> variant in $LIBS (scripts/build_variant.sh; timing-only
 # experiment builds allowed). TESTS=1 first runs the lap kernel's GPU parity
 # tests on the in-tree package.
 set -o pipefail
@@ -12,7 +12,7 @@ if [ -n "$TESTS" ]; then
 fi
 S=${SPECS:-"64x16x64:TSA_LAP_M=1,TSA_LAP_NW=8,TSA_LAP_SINGLE=1 64x8x64:TSA_LAP_M=1,TSA_LAP_NW=4,TSA_LAP_SINGLE=1 64:TSA_LAP_M=1,TSA_LAP_NW=8 64:TSA_LAP_M=1,TSA_LAP_NW=4"}
 for which in cur ${LIBS}; do
-  if [ $which = cur ]; then unset TSA_PKG_DIR; else export TSA_PKG_DIR=$GRAFT_REPO_ROOT/scratch/$which; fi
+  if [ $which = cur ]; then unset TSA_PKG_DIR; else export TSA_PKG_DIR=$GRAFT_REPO_ROOT/variants/$which; fi
   timeout -k 10 200 python tools/lap_trace.py $S > gpurun_out/lapvar_$which.jsonl 2> gpurun_out/lapvar_$which.err
   rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/lapvar_$which.err; exit $rc; }
   echo "== $which"; python -c "

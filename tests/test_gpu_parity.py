@@ -160,16 +160,32 @@ def test_pencil_wide_positions(gpu, orc, monkeypatch, mode):
     assert gpu.score(a, b, c, p, kernel="pencil") == orc.score(a, b, c, op), mode
 
 
-@pytest.mark.parametrize("nw", ["8", "16"])
-def test_pencil_waves_per_workgroup(gpu, orc, monkeypatch, nw):
-    monkeypatch.setenv("TSA_PENCIL_NW", nw)
-    rng = np.random.default_rng(int(nw))
-    for la, lb, lc in [(256, 40, 256), (100, 9, 130), (33, 70, 64), (300, 25, 255)]:
-        a, b, c = (rng.integers(0, 5, n).astype(np.uint8) for n in (la, lb, lc))
-        assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (nw, la, lb, lc)
+@pytest.mark.parametrize("s3_mode", [0, 1])
+def test_vspace_helix(gpu, orc, monkeypatch, s3_mode):
+    """The helix's V-space cell (values shifted by lam*(x+y+z), faces injected
+    as lam*q; tests/test_cell_algebra.py replays the algebra): ragged batches
+    that wrap laps at every phase of the four-step loop, TWO mode (LC <= 64),
+    M = 1 and 2, the last wave's early face records, lam = 1 and lam = 2."""
+    monkeypatch.setenv("TSA_PENCIL_MODE", "helix")
+    rng = np.random.default_rng(70 + s3_mode)
+    for kw in [dict(), dict(match=2, mismatch=-2, gap_open=3, gap_extend=2)]:
+        kw = dict(kw, s3_mode=s3_mode)
+        p, op = gpu.TsaParams.default(**kw), orc.default_params(**kw)
+        for n, hi in ((9, (200, 40, 250)), (21, (100, 30, 64)), (5, (260, 19, 129))):
+            triples = [tuple(rng.integers(0, 5, int(rng.integers(1, h + 1))).astype(np.uint8) for h in hi)
+                       for _ in range(n)]
+            ml = [max(len(t[k]) for t in triples) for k in range(3)]
+            assert " f16v " in gpu.describe_plan(n, *ml, p, sync=True), (kw, ml)
+            seqs, offs = gpu.pack_batch(triples)
+            got = gpu.score_batch(triples, p)
+            assert np.array_equal(got, orc.score_batch(seqs, offs, op, nthreads=8)), (kw, ml)
+    # all-match (the V-space bound's top) and all-distinct triples
+    p = gpu.TsaParams.default()
+    for a, b, c in ((np.zeros(256, np.uint8),) * 3, tuple(np.full(200, v, np.uint8) for v in (0, 1, 2))):
+        assert gpu.score_batch([(a, b, c)] * 3, p)[0] == orc.score(a, b, c)
 
 
-@pytest.mark.parametrize("arith", ["f16", "i16"])
+@pytest.mark.parametrize("arith", ["f16v", "f16", "i16"])
 @pytest.mark.parametrize("s3_mode", [0, 1])
 def test_pencil_arithmetic_forms(gpu, orc, monkeypatch, arith, s3_mode):
     # helix kernel: exact-f16 (default where the value bound allows) and int16
@@ -217,7 +233,7 @@ def test_pencil_single_cube_modes(gpu, orc, synth, monkeypatch, mode):
         assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (mode, la, lb, lc)
 
 
-@pytest.mark.parametrize("nw", ["8", "16"])
+@pytest.mark.parametrize("nw", ["4", "8"])
 def test_pencil_lap_rows_per_lap(gpu, orc, synth, monkeypatch, nw):
     monkeypatch.setenv("TSA_LAP_NW", nw)
     rng = np.random.default_rng(40 + int(nw))
@@ -226,13 +242,15 @@ def test_pencil_lap_rows_per_lap(gpu, orc, synth, monkeypatch, nw):
         assert gpu.score(a, b, c, kernel="pencil") == orc.score(a, b, c), (nw, la, lb, lc)
 
 
-@pytest.mark.parametrize("zt", ["128", "256", "512"])
-def test_pencil_lap_z_tiles(gpu, orc, monkeypatch, zt):
-    # single-cube lap kernel with the z axis cut into 128*M-position tiles that
-    # hand their last position to the next tile's position 0 every step;
-    # partial last tiles, one-lap cubes, LA below/above the tile width
-    monkeypatch.setenv("TSA_LAP_ZT", zt)
-    rng = np.random.default_rng(60 + int(zt))
+@pytest.mark.parametrize("m", ["1", "2", "4"])
+def test_pencil_lap_z_tiles(gpu, orc, monkeypatch, m):
+    # single-cube lap kernel with the z axis cut into 64*M-position tiles (M
+    # packed pairs per lane) that hand their last position to the next tile's
+    # position 0 every step; partial last tiles, one-lap cubes, LA below/above
+    # the tile width
+    monkeypatch.setenv("TSA_PENCIL_MODE", "lap")
+    monkeypatch.setenv("TSA_LAP_M", m)
+    rng = np.random.default_rng(60 + int(m))
     p, op = gpu.TsaParams.default(score_bits=16), orc.default_params(score_bits=16)
     for la, lb, lc in [(300, 16, 300), (130, 40, 260), (150, 16, 129), (64, 17, 130),
                        (256, 48, 256), (40, 33, 513), (520, 20, 700)]:
@@ -242,7 +260,7 @@ def test_pencil_lap_z_tiles(gpu, orc, monkeypatch, zt):
         c = a[:lc].copy()
         c[::9] = (c[::9] + 2) % 4  # related sequences: long matching runs
         assert gpu.score(a[:la], b, c, p, kernel="pencil") == orc.score(a[:la], b, c, op), \
-            (zt, la, lb, lc)
+            (m, la, lb, lc)
 
 
 def test_pencil_lap_mode_small_batch(gpu, orc):

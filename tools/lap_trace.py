@@ -135,7 +135,7 @@ def main():
                 "bp_waits": sum(int(r["bp_waits"]) for r in rows),
             })
             prof_cols = [k for k in rows[0] if k.startswith("prof")]
-            if prof_cols:  # TSA_LAP_PROF build: per-wave cycles per step (medians over workgroups)
+            if prof_cols:  # TSA_DIAG build: per-wave cycles per step (medians over workgroups)
                 prof = {}
                 for wv in range(NW):
                     parts = []
