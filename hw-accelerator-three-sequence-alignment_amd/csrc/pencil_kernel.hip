@@ -363,9 +363,11 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       return h_bits(pa.lam * (lp * NW + w + 1 + (u - lp * P)));
     };
     if constexpr (VS) {
-      Hr[3] = h_at(-1);
       Hr[0] = h_at(0);
       Hr[1] = h_at(1);
+      // the step-0 injection's (0, y-1, z-1) face is H(0) - lam (wave 0 starts
+      // its first row at step 0 with no wrap that would have set it)
+      Hr[3] = U(H(Hr[0]) - H(pa.v_lam));
     }
     // wave 0: prime the LDS-DMA pipeline (ring row of step s = s - P + NW - 1)
     if (w == 0) {
