@@ -1,6 +1,8 @@
-"""The pencil kernel's schedule (helix positions, systolic shifts, LDS record
-hand-off, global ring with face rows) replayed on CPU by tools/pencil_emu.py
-must reproduce the oracle. Guards the algorithm independently of the GPU."""
+"""The helix kernel's schedule (positions, the two-step wave skew, LDS record
+slots, the wave-0 ring with its face rows, x = 1 injection, z-shifts, TWO mode)
+replayed on CPU by tools/pencil_emu.py must reproduce the oracle, in the
+message form and in the V-space form (values shifted by lam*(x+y+z), faces
+injected as lam*q). Guards the algorithm independently of the GPU."""
 import os
 import sys
 
@@ -10,14 +12,35 @@ import pytest
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
 
 
-@pytest.mark.parametrize("skew", [1, 2])
-@pytest.mark.parametrize("la,lb,lc,sop", [(64, 64, 64, 0), (47, 17, 128, 1), (60, 1, 65, 0),
-                                          (130, 20, 200, 0), (5, 40, 3, 1), (300, 3, 40, 0)])
-def test_emulated_schedule_matches_oracle(orc, la, lb, lc, sop, skew):
-    # skew 2 is the kernel's M <= 2 schedule (waves two steps apart, four
-    # record slots per wave), skew 1 its M >= 4 one
+@pytest.mark.parametrize("vs", [False, True])
+@pytest.mark.parametrize("la,lb,lc,sop", [(64, 20, 64, 0), (47, 17, 128, 1), (60, 1, 65, 0),
+                                          (130, 12, 200, 0), (5, 19, 3, 1), (300, 3, 40, 0),
+                                          (8, 8, 8, 0)])
+def test_emulated_schedule_matches_oracle(orc, la, lb, lc, sop, vs):
     import pencil_emu
     rng = np.random.default_rng(la * 1000 + lb * 10 + lc)
     a, b, c = (rng.integers(0, 5, n) for n in (la, lb, lc))
-    got = pencil_emu.emulate(a, b, c, sop=bool(sop), skew=skew)
-    assert got == orc.score(a, b, c, orc.default_params(s3_mode=sop))
+    got = pencil_emu.emulate([(a, b, c)], sop=bool(sop), vs=vs)
+    assert got == [orc.score(a, b, c, orc.default_params(s3_mode=sop, score_bits=0))]
+
+
+@pytest.mark.parametrize("vs", [False, True])
+def test_emulated_two_triples(orc, vs):
+    """TWO mode (LC <= 64): the halves of every register score two triples of
+    different lengths at the same positions."""
+    rng = np.random.default_rng(3)
+    t1 = tuple(rng.integers(0, 4, n) for n in (40, 13, 64))
+    t2 = tuple(rng.integers(0, 4, n) for n in (70, 9, 30))
+    import pencil_emu
+    got = pencil_emu.emulate([t1, t2], vs=vs)
+    p = orc.default_params(score_bits=0)
+    assert got == [orc.score(*t1, p), orc.score(*t2, p)]
+
+
+def test_emulated_vspace_lam2(orc):
+    kw = dict(match=2, mismatch=-2, go=3, ge=2)
+    import pencil_emu
+    rng = np.random.default_rng(11)
+    a, b, c = (rng.integers(0, 4, n) for n in (50, 11, 90))
+    p = orc.default_params(score_bits=0, match=2, mismatch=-2, gap_open=3, gap_extend=2)
+    assert pencil_emu.emulate([(a, b, c)], vs=True, **kw) == [orc.score(a, b, c, p)]

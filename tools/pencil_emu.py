@@ -1,124 +1,210 @@
-"""CPU emulation of the pencil kernel's schedule (pencil_kernel.hip) -- a
-debugging aid. Arrays are [wave][lane][pair][half] int32; every step mirrors
-the kernel's receive / substitute / compute / send / shift sequence, with the
-same helix position mapping k = 64*M*half + M*lane + pair."""
-import sys
+"""CPU replay of the helix kernel's schedule (csrc/pencil_kernel.hip).
+
+TEST/DESIGN INFRASTRUCTURE: the helix's index and timing logic -- positions,
+halves, the two-step wave skew, LDS record slots, the wave-0 ring with its
+face rows, x = 1 injection, z-shifts with the z = 0 face, the final-cell
+capture -- executed register by register with exact integer arithmetic, in
+the message form (`vs=False`) or the V-space form of cell_messages_vs
+(`vs=True`: values shifted by lam*(x+y+z), faces lam*q). tests/
+test_pencil_schedule.py checks it against the oracle.
+
+Layout as in the kernel: NW = 8 waves, wave w owns row y = lap*NW + w + 1;
+lane l, register i, half h is position k = 64M h + M l + i (TWO mode, LC <= 64
+and M = 1: k = l, and half h scores its own triple); position k of wave w
+computes x = (t - S w - k) mod P + 1 at step t (S = 2).
+"""
+from __future__ import annotations
+
 import numpy as np
 
-PD, PMIN, NW = 8, 48, 16
+NW, S, RING_EXTRA = 8, 2, 8
 
 
-def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, skew=1):
-    # skew: steps between consecutive waves (TSA_SKEW; the kernel uses 2 for
-    # M <= 2): wave w reads wave w-1's record of step t-skew from 2*skew slots
-    la, lb, lc = len(a), len(b), len(c)
-    M = 1 if lc <= 128 else 2
-    ZT = 128 * M
-    P = max(la, ZT, PMIN)
-    R = P + 8
-    E, O, E2, OE, O2 = ge, go, 2 * ge, go + ge, 2 * go
-    f_single = -min(E2, OE, O2)
-    f_pair = -min(E, O)
-    oh = lambda s: 1 << (int(s) & 3)
-    sA = np.array([oh(a[i]) if i < la else 0 for i in range(P)])
-    sB = np.array([oh(b[i]) if i < lb else 0 for i in range(4096)])
-    lane = np.arange(64)
-    k = M * lane[:, None, None] + 64 * M * np.arange(2)[None, None, :] + np.arange(M)[None, :, None]  # [64][M][2]
-    cpos = np.where(k < lc, np.array([oh(c[j]) if j < lc else 0 for j in range(ZT)])[np.minimum(k, ZT - 1)], 0)
-    W = np.arange(NW)[:, None, None, None]
-    shape = (NW, 64, M, 2)
-    x0 = ((-W - k[None]) % P)
-    areg = sA[x0]
-    breg = np.zeros(shape, np.int64)
-    breg[0, 0, 0, 0] = sB[0]
-    oIx = np.full(shape, f_single); shIz = np.full(shape, f_single)
-    shIxz1 = np.full(shape, f_pair); shIxz2 = np.full(shape, f_pair)
-    svIxy = np.full(shape, f_pair); svIyz = np.full(shape, f_pair)
-    svM1 = np.zeros(shape, np.int64); svM2 = np.zeros(shape, np.int64)
-    xr = np.zeros((NW, 2 * skew, 64, M, 2, 4), np.int64)   # record slots written by wave w
-    ring = np.zeros((R, 64, M, 2, 4), np.int64)
-    ring[..., 0] = f_single; ring[..., 1] = f_pair; ring[..., 2] = f_pair; ring[..., 3] = 0
-    lap = P - skew * (NW - 1)
-    xpos0 = np.array([(P - (skew * w % P)) % P for w in range(NW)])
-    lap0 = np.array([0 if w == 0 else -1 for w in range(NW)])
-    lap_f, w_f, k_f = (lb - 1) // NW, (lb - 1) % NW, lc - 1
-    t_f = lap_f * P + (la - 1) + skew * w_f + k_f
-    h_f = k_f // (64 * M); l_f, i_f = divmod(k_f - 64 * M * h_f, M)
-    order = np.argsort(k.reshape(-1))  # flat (lane, pair, half) index of position 0, 1, ...
+def penalties(go, ge):
+    GO2, GE2, GOGE = 2 * go, 2 * ge, go + ge
+    return np.array([[0, 0, 0, 0, 0, 0, 0],
+                     [GO2, GE2, GOGE, GOGE, GOGE, GO2, GOGE],
+                     [GO2, GOGE, GE2, GOGE, GOGE, GOGE, GO2],
+                     [GO2, GOGE, GOGE, GE2, GO2, GOGE, GOGE],
+                     [go, ge, ge, go, ge, go, go],
+                     [go, go, ge, ge, go, ge, go],
+                     [go, ge, go, ge, go, go, ge]], dtype=np.int64)
 
-    def shift(v, inj):
-        # position k <- k-1 along the helix; position 0 gets inj (per wave)
-        flat = v.reshape(v.shape[0], -1)
-        out = np.empty_like(flat)
-        out[:, order[1:]] = flat[:, order[:-1]]
-        out[:, order[0]] = inj
-        return out.reshape(v.shape)
 
-    score = None
-    for t in range(t_f + 1):
-        rec = np.empty((NW, 64, M, 2, 4), np.int64)
-        rec[0] = ring[(t - lap) % R]
-        rec[1:] = xr[:-1, (t - skew) % (2 * skew)]
-        inIx, inIy, inIz = oIx.copy(), rec[..., 0].copy(), shIz.copy()
-        inIxy, inIyz, inIxz, inM = svIxy.copy(), svIyz.copy(), shIxz2.copy(), svM2.copy()
+def emulate(triples, match=1, mismatch=-1, go=2, ge=1, sop=False, vs=False):
+    """Scores of one workgroup's unit: one triple, or two (TWO mode: LC <= 64).
+    Returns a list of scores (one per triple)."""
+    two = len(triples) == 2
+    la_, lb_, lc_ = ([len(t[k]) for t in triples] for k in range(3))
+    max_la, max_lb, max_lc = max(la_), max(lb_), max(lc_)
+    M = 1 if max_lc <= 128 else 2
+    assert not two or max_lc <= 64
+    KS = 64 if two else 128 * M
+    P = max(max_la, 64 if two else 128 * M)
+    P = -(-P // M) * M
+    R = P + RING_EXTRA
+    lam = ge if vs else 0
+    assert not vs or ge == -mismatch
+    Pen = penalties(go, ge)
+    f_single, f_pair = -int(Pen[1].min()), -int(Pen[4].min())
+    dm = match - mismatch
+    lanes = np.arange(64)
+    shape = (M, 64, 2)
+    i_ = np.arange(M)[:, None, None]
+    l_ = lanes[None, :, None]
+    h_ = np.arange(2)[None, None, :]
+    kpos = (l_ + 0 * h_ + 0 * i_) if two else (64 * M * h_ + M * l_ + i_)   # [M, 64, 2]
+    tri_of = (h_ + 0 * l_ + 0 * i_) if two else np.zeros(shape, np.int64)
+    trip = triples if two else triples * 2
+
+    def code(seq, idx):  # symbol (mod 4) or -1 past the sequence
+        seq = np.asarray(seq, np.int64)
+        ok = (idx >= 0) & (idx < len(seq))
+        return np.where(ok, seq[np.clip(idx, 0, max(len(seq) - 1, 0))] & 3 if len(seq) else -1, -1)
+
+    def per_half(fn):
+        out = np.empty(shape, np.int64)
+        for h in range(2):
+            out[..., h] = fn(trip[h], h)[..., h]
+        return out
+
+    ccode = per_half(lambda t, h: code(t[2], kpos))
+    # final cells: t_f per triple
+    t_fs, w_fs, k_fs = [], [], []
+    for (a, b, c) in (triples if two else triples[:1]):
+        la, lb, lc = len(a), len(b), len(c)
+        t_fs.append(((lb - 1) // NW) * P + (la - 1) + S * ((lb - 1) % NW) + (lc - 1))
+        w_fs.append((lb - 1) % NW)
+        k_fs.append(lc - 1)
+    T = max(t_fs) + 1
+    lag = P - S * (NW - 1)
+    fin = [None] * len(t_fs)
+
+    def face_rec(tr):  # the y = 0 row as wave 0 meets it at step tr
+        if vs:
+            return np.array([lam * (tr + 1), lam * (tr + 2), lam * (tr + 2), lam * (tr + 2)])
+        return np.array([f_single, f_pair, f_pair, 0])
+
+    ring = np.stack([face_rec((r + lag) % R)[:, None, None, None] * np.ones((1,) + shape, np.int64)
+                     for r in range(R)])          # [R, 4, M, 64, 2]
+    xr = np.zeros((NW, 4, 4) + shape, np.int64)    # [wave][slot][field]
+    st = []
+    for w in range(NW):
+        xpos0 = (P - (S * w) % P) % P
+        lap0 = 0 if w == 0 else -1
+        d = dict(oIx=np.full(shape, f_single), shIz=np.full(shape, f_single),
+                 svIxy=np.full(shape, f_pair), svIyz=np.full(shape, f_pair),
+                 shIxz=[np.full(shape, f_pair), np.full(shape, f_pair)],
+                 svM=[np.zeros(shape, np.int64), np.zeros(shape, np.int64)],
+                 b=np.full(shape, -1), xpos0=xpos0, lap0=lap0)
+        if vs:  # H(s) = lam (y + xpos0) at step s, H(-1) := H(0) - lam
+            def h_at(s, w=w):
+                u = s - S * w
+                lp = u // P
+                return lam * (lp * NW + w + 1 + (u - lp * P))
+            d["H"] = {0: h_at(0), 1: h_at(1), -1: h_at(0) - lam}
+        st.append(d)
+
+    def shift(v, face):
+        # position k <- k-1; lane 0 register 0: low half the face, high half
+        # lane 63's low half of register M-1 (TWO: both halves the face)
+        out = np.empty_like(v)
+        out[1:] = v[:-1]
+        out[0, 1:] = v[M - 1, :-1]
+        out[0, 0, 0] = face
+        out[0, 0, 1] = face if two else v[M - 1, 63, 0]
+        return out
+
+    for t in range(T):
+        PH = t & 1
+        outs = [None] * NW
         for w in range(NW):
-            ks = xpos0[w]
-            if ks < ZT:
-                h = ks // (64 * M); l, i = divmod(ks - 64 * M * h, M)
-                inIx[w, l, i, h] = f_single; inIxy[w, l, i, h] = f_pair
-                inIxz[w, l, i, h] = f_pair; inM[w, l, i, h] = 0
-        eab = (areg & breg) != 0
-        eac = (areg & cpos[None]) != 0
-        ebc = (breg & cpos[None]) != 0
-        s2 = lambda e: np.where(e, match, mismatch)
-        s2ab, s2ac, s2bc = s2(eab), s2(eac), s2(ebc)
-        if sop:
-            s3 = s2ab + s2bc + s2ac
-        else:
-            s3 = np.where(eab, np.where(ebc, 3 * match, 2 * (match + mismatch)), 3 * mismatch)
-        sM = inM + s3; sX, sY, sZ = inIx, inIy, inIz
-        sXY, sYZ, sXZ = inIxy + s2ab, inIyz + s2bc, inIxz + s2ac
-        mx = np.maximum
-        # GO >= GE: each target's highest-penalty group widened to all 7 states
-        best = mx.reduce([sM, sX, sY, sZ, sXY, sYZ, sXZ])
-        nIx = mx.reduce([sX - E2, mx.reduce([sY, sZ, sXY, sXZ]) - OE, best - O2])
-        oIy = mx.reduce([sY - E2, mx.reduce([sX, sZ, sXY, sYZ]) - OE, best - O2])
-        oIz = mx.reduce([sZ - E2, mx.reduce([sX, sY, sYZ, sXZ]) - OE, best - O2])
-        oIxy = mx(mx.reduce([sX, sY, sXY]) - E, best - O)
-        oIyz = mx(mx.reduce([sY, sZ, sYZ]) - E, best - O)
-        oIxz = mx(mx.reduce([sX, sZ, sXZ]) - E, best - O)
-        recout = np.stack([oIy, oIxy, oIyz, best], -1)
-        xr[:, t % (2 * skew)] = recout
-        last = recout[NW - 1].copy()
-        unstarted = (t - skew * (NW - 1) - k) < 0   # u < 0: row y0-1 of lap 0 is the y=0 face
-        last[unstarted] = [f_single, f_pair, f_pair, 0]
-        ring[t % R] = last
-        if t == t_f:
-            score = int(best[w_f, l_f, i_f, h_f])
-        oIx = nIx
-        shIxz2 = shIxz1
-        shIxz1 = shift(oIxz, f_pair)
-        shIz = shift(oIz, f_single)
-        svIxy = rec[..., 1]
-        svIyz = shift(rec[..., 2], f_pair)
-        svM2 = svM1
-        svM1 = shift(rec[..., 3], 0)
-        xpos0 = xpos0 + 1
-        wrap = xpos0 == P
-        xpos0[wrap] = 0; lap0[wrap] += 1
-        ainj = sA[xpos0]
-        row0 = lap0 * NW + np.arange(NW)
-        binj = np.where((lap0 >= 0) & (row0 < lb), sB[np.clip(row0, 0, 4095)], 0)
-        ash = shift(areg, 0); ash[:, 0, 0, 0] = ainj; areg = ash
-        bsh = shift(breg, 0); bsh[:, 0, 0, 0] = binj; breg = bsh
-    return score
-
-
-if __name__ == "__main__":
-    sys.path.insert(0, "oracle")
-    import oracle
-    rng = np.random.default_rng(0)
-    for la, lb, lc in [(64, 64, 64), (5, 40, 3), (47, 17, 128), (130, 31, 200), (20, 3, 1)]:
-        A, B, C = (rng.integers(0, 4, n) for n in (la, lb, lc))
-        e, r = emulate(A, B, C), oracle.score(A, B, C)
-        print(la, lb, lc, e, r, "OK" if e == r else "MISMATCH")
+            d = st[w]
+            rec = ring[(t - lag) % R] if w == 0 else xr[w - 1, (t - S) & 3]
+            u = (t - S * w - kpos) % P
+            acode = per_half(lambda tr, h: code(tr[0], u))
+            inIx, inIy, inIz = d["oIx"].copy(), rec[0].copy(), d["shIz"].copy()
+            inIxy, inIyz = d["svIxy"].copy(), d["svIyz"].copy()
+            inIxz, inM = d["shIxz"][PH].copy(), d["svM"][PH].copy()
+            b = d["b"]
+            if d["xpos0"] < KS:  # x = 1 at position xpos0: the x = 0 face, the row's B
+                inj = kpos == d["xpos0"]
+                row = d["lap0"] * NW + w
+                bn = per_half(lambda tr, h: code(tr[1], np.full(shape, row)))
+                b = np.where(inj, bn, b)
+                d["b"] = b
+                if vs:
+                    inIx[inj] = inIxy[inj] = inIxz[inj] = d["H"][t]
+                    inM[inj] = d["H"][t - 1]
+                else:
+                    inIx[inj], inIxy[inj], inIxz[inj], inM[inj] = f_single, f_pair, f_pair, 0
+            eab = (acode >= 0) & (acode == b)
+            eac = (acode >= 0) & (acode == ccode)
+            ebc = (b >= 0) & (b == ccode)
+            if vs:
+                sXY, sXZ, sYZ = inIxy + dm * eab, inIxz + dm * eac, inIyz + dm * ebc
+                if sop:
+                    sM = inM + dm * (eab.astype(np.int64) + ebc + eac) + 3 * mismatch + 3 * lam
+                else:
+                    sM = inM + np.where(eab, np.where(ebc, 3 * match, 2 * (match + mismatch)) - 3 * mismatch,
+                                        0) + 3 * mismatch + 3 * lam
+                sX, sY, sZ = inIx, inIy, inIz
+                mx = np.maximum
+                Gx, Gy, Gz = mx(mx(sY, sZ), sYZ), mx(mx(sX, sZ), sXZ), mx(mx(sX, sY), sXY)
+                best = mx(mx(Gx, Gy), mx(sXY, sM))
+                b1 = best - (go - ge)
+                pXY, pYZ, pXZ = mx(Gz, b1), mx(Gx, b1), mx(Gy, b1)
+                cP = go + mismatch + lam
+                nIx = mx(sX - lam, mx(pXY, pXZ) - cP)
+                oIy = mx(sY - lam, mx(pXY, pYZ) - cP)
+                oIz = mx(sZ - lam, mx(pYZ, pXZ) - cP)
+                oIxy, oIyz, oIxz = pXY, pYZ, pXZ
+            else:  # message form, mismatch not folded (integer arithmetic)
+                s2 = lambda e: np.where(e, match, mismatch)
+                if sop:
+                    s3 = s2(eab) + s2(ebc) + s2(eac)
+                else:
+                    s3 = np.where(eab, np.where(ebc, 3 * match, 2 * (match + mismatch)), 3 * mismatch)
+                Sst = np.stack([inM + s3, inIx, inIy, inIz, inIxy + s2(eab), inIyz + s2(ebc),
+                                inIxz + s2(eac)])
+                msg = [(Sst - Pen[T_][:, None, None, None]).max(0) for T_ in range(7)]
+                best, nIx, oIy, oIz, oIxy, oIyz, oIxz = msg
+            for j, (tf, wf, kf) in enumerate(zip(t_fs, w_fs, k_fs)):
+                if t == tf and w == wf:
+                    pos = np.argwhere((kpos == kf) & (tri_of == j))[0]
+                    fin[j] = int(best[tuple(pos)])
+            out = np.stack([oIy, oIxy, oIyz, best])
+            if w == NW - 1 and t < KS + S * NW:  # not-started positions publish the y = 0 face
+                unstarted = kpos > t - S * w
+                fr = face_rec(t + lag)
+                for f in range(4):
+                    out[f][unstarted] = fr[f]
+            outs[w] = out
+            # advance: position 0 moves on (wrap: a new row), then the z-shifts
+            d["oIx"] = nIx
+            d["svIxy"] = rec[1]
+            if vs:
+                d["H"][t + 2] = d["H"][t + 1] + lam
+            d["xpos0"] += 1
+            if d["xpos0"] == P:
+                d["xpos0"] = 0
+                d["lap0"] += 1
+                if vs:
+                    y = d["lap0"] * NW + w + 1
+                    d["H"][t], d["H"][t + 1], d["H"][t + 2] = lam * (y - 1), lam * y, lam * (y + 1)
+            if vs:
+                h1, h2 = d["H"][t + 1], d["H"][t + 2]
+                d["shIxz"][PH] = shift(oIxz, h2)
+                d["shIz"] = shift(oIz, h1)
+                d["svIyz"] = shift(rec[2], h1)
+                d["svM"][PH] = shift(rec[3], h1)
+            else:
+                d["shIxz"][PH] = shift(oIxz, f_pair)
+                d["shIz"] = shift(oIz, f_single)
+                d["svIyz"] = shift(rec[2], f_pair)
+                d["svM"][PH] = shift(rec[3], 0)
+        for w in range(NW):
+            xr[w, t & 3] = outs[w]
+        ring[t % R] = outs[NW - 1]
+    shifts = [lam * (len(a) + len(b) + len(c)) for (a, b, c) in (triples if two else triples[:1])]
+    return [f - s for f, s in zip(fin, shifts)]
