@@ -1,0 +1,503 @@
+// literal_kernel.hip -- the RTL's literal arithmetic in the helix schedule
+// (TSA_KERNEL_PLANE's batch path; tools/literal_emu.py replays it on the CPU).
+//
+// The literal recurrence (src/PE_1cyc.v:164-218) wraps every one of a target's
+// 7 candidates to SCORE_BITS before the MAX7 (the `wordsize` candidate wires,
+// src/PE_1cyc.v:127-133), so it cannot be factored into messages the way the
+// pencil kernels do. In PULL form a cell needs all 7 states of 7 predecessors;
+// in PUSH form it needs only its own 7 states and its successors' symbols
+// (a_{x+1}, b_{y+1}, c_{z+1}): for each successor it computes the one state
+// that successor takes from it -- the full literal MAX7 -- and sends it. The
+// data flow is then exactly the helix's (pencil_kernel.hip): one value per
+// edge, {Iy, Ixy, Iyz, M} records down the rows, {Ix} along x, {Iz, Ixz, Iyz,
+// M} shifted along z, so the same schedule runs it:
+//   * one workgroup per triple, NW = 8 waves = rows, two steps of skew per row,
+//     one s_barrier per two steps, the wave-0 ring prefetched by LDS-DMA;
+//   * lane l, register i, half h is position k = 64M h + M l + i (z = k + 1);
+//   * position k of wave w is at x' = (t - 2w - k) mod P at step t: x' = 0 is a
+//     column of the helix for the x = 0 face (P >= LA + 1) -- that position's 7
+//     inputs are forced to 0, so its pushes are the face's;
+//   * the y = 0 face: ring rows wave 0 reads in its first lap hold row 0's
+//     pushes into row 1; the z = 0 face: position 0's z-1 inputs are pushes of
+//     a zero cell with its own symbols (a_x, b_y, c_1), chosen in SALU.
+// Arithmetic: every value shifted left by 16 - SCORE_BITS in an int16 half
+// (two cells per VGPR), so v_pk_add_u16 wraps exactly at the RTL word and
+// v_pk_max_i16 is its signed compare: no wrap instruction at all. Per cell pair
+// 94 VALU: 28 for the three single targets (13 shared candidate adds), 15 for
+// each pair target and M, 6 for the successor indicators.
+
+#include "pencil_common.h"
+
+namespace tsa {
+
+// Scaled constants (value << sh as int16, both halves).
+struct LitArgs {
+  uint32_t n2E, nOE, n2O;   // -2GE, -(GO+GE), -2GO
+  uint32_t dmS, mmE, nDOE;  // match - mismatch, mismatch - GE, -(GO - GE)
+  uint32_t d1S, d0S, neS;   // RTL s3 = ne + [a=b](d0 + [b=c] d1)
+  uint32_t mm3S;            // SOP s3 = 3 mismatch + dm ([a=b] + [b=c] + [a=c])
+  // pushes of a zero cell (the faces): to Ix / Iy / Iz, to a pair target with
+  // its pair score a match (1) or not (0), to M by the successor's indicators
+  uint32_t fS[3], fP[2], fM[8];
+  int32_t sh, packed;
+};
+
+constexpr int LIT_NW = 8, LIT_S = 2, LIT_PD = 8, LIT_RING_EXTRA = 8;
+
+struct LitGeom {
+  int32_t M, P, R;
+  int64_t ring_bytes_per_triple;
+  size_t lds;
+};
+static LitGeom lit_geom(int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  LitGeom g;
+  g.M = max_lc <= 128 ? 1 : 2;
+  g.P = std::max(max_la + 1, 128 * g.M);  // x' = 0 .. LA: the face column first
+  g.P = (g.P + g.M - 1) / g.M * g.M;       // M = 2: the x' = 0 register is (t - w) parity
+  g.R = g.P + LIT_RING_EXTRA;
+  g.ring_bytes_per_triple = (int64_t)g.R * g.M * 64 * REC_BYTES;
+  g.lds = (size_t)(LIT_NW - 1) * 2 * LIT_S * g.M * 1024 + (size_t)LIT_PD * g.M * 1024 +
+          4 * ((size_t)g.P + 128 * g.M) + 4 * (((size_t)max_lb + 4) & ~(size_t)3) + (size_t)7 * g.M * 256 + 32;
+  return g;
+}
+
+bool literal_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  if (max_la < 1 || max_lb < 1 || max_lc < 1 || max_lc > 256 || max_la > 4095 || max_lb > 4096) return false;
+  return lit_geom(max_la, max_lb, max_lc).lds <= LDS_MAX;
+}
+bool literal_helix_chosen(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  if (!literal_shape_ok(max_la, max_lb, max_lc)) return false;
+  if (const char *e = getenv("TSA_PENCIL_MODE")) {
+    if (!strcmp(e, "plane")) return false;
+    if (!strcmp(e, "literal")) return true;
+  }
+  return n >= 16;  // a single cube runs faster as a plane sweep over the whole chip
+}
+size_t literal_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  return (size_t)std::min<int32_t>(n, 65535) * (size_t)lit_geom(max_la, max_lb, max_lc).ring_bytes_per_triple;
+}
+
+__device__ __forceinline__ uint32_t add2(uint32_t a, uint32_t b) { return pk_add(a, b); }
+__device__ __forceinline__ uint32_t mx2(uint32_t a, uint32_t b) { return pk_max(a, b); }
+
+// The 7 states a cell with states (M, X, Y, Z, XY, YZ, XZ) pushes to its
+// successors (src/PE_1cyc.v:164-218 with the successor's scores): nIx to
+// (x+1,y,z), oIy (x,y+1,z), oIz (x,y,z+1), oIxy (x+1,y+1,z), oIyz (x,y+1,z+1),
+// oIxz (x+1,y,z+1), oM (x+1,y+1,z+1). an/bn/cn: the successors' symbol codes.
+template <bool SOP>
+__device__ __forceinline__ void push_literal(const LitArgs &c, uint32_t ones, uint32_t MM, uint32_t X,
+                                             uint32_t Y, uint32_t Z, uint32_t XY, uint32_t YZ,
+                                             uint32_t XZ, uint32_t an, uint32_t bn, uint32_t cn,
+                                             uint32_t &nIx, uint32_t &oIy, uint32_t &oIz, uint32_t &oIxy,
+                                             uint32_t &oIyz, uint32_t &oIxz, uint32_t &oM) {
+  // single targets: the 13 distinct wrapped candidates, shared
+  const uint32_t m2O = add2(MM, c.n2O);
+  const uint32_t x2E = add2(X, c.n2E), xOE = add2(X, c.nOE);
+  const uint32_t y2E = add2(Y, c.n2E), yOE = add2(Y, c.nOE);
+  const uint32_t z2E = add2(Z, c.n2E), zOE = add2(Z, c.nOE);
+  const uint32_t xyOE = add2(XY, c.nOE), xy2O = add2(XY, c.n2O);
+  const uint32_t yzOE = add2(YZ, c.nOE), yz2O = add2(YZ, c.n2O);
+  const uint32_t xzOE = add2(XZ, c.nOE), xz2O = add2(XZ, c.n2O);
+  const uint32_t A = mx2(mx2(m2O, zOE), xyOE), Bv = mx2(xOE, yzOE);
+  nIx = mx2(mx2(A, x2E), mx2(mx2(yOE, yz2O), xzOE));            // :172-178
+  oIy = mx2(mx2(A, Bv), mx2(y2E, xz2O));                         // :180-186
+  oIz = mx2(mx2(Bv, m2O), mx2(mx2(yOE, z2E), mx2(xy2O, xzOE)));  // :188-194
+  // the successors' pair scores (src/PE_1cyc.v:159-161), as (s2 - GE) and (s2 - GO)
+  const uint32_t eab = pk_eq1(an, bn, ones), ebc = pk_eq1(bn, cn, ones), eac = pk_eq1(an, cn, ones);
+  const uint32_t uxy = pk_mad(eab, c.dmS, c.mmE), vxy = add2(uxy, c.nDOE);
+  const uint32_t uyz = pk_mad(ebc, c.dmS, c.mmE), vyz = add2(uyz, c.nDOE);
+  const uint32_t uxz = pk_mad(eac, c.dmS, c.mmE), vxz = add2(uxz, c.nDOE);
+  // pair targets: penalty GE from the states sharing the gap, GO from the rest
+  oIxy = mx2(mx2(mx2(add2(X, uxy), add2(Y, uxy)), mx2(add2(XY, uxy), add2(MM, vxy))),   // :196-202
+             mx2(mx2(add2(Z, vxy), add2(YZ, vxy)), add2(XZ, vxy)));
+  oIyz = mx2(mx2(mx2(add2(Y, uyz), add2(Z, uyz)), mx2(add2(YZ, uyz), add2(MM, vyz))),   // :204-210
+             mx2(mx2(add2(X, vyz), add2(XY, vyz)), add2(XZ, vyz)));
+  oIxz = mx2(mx2(mx2(add2(X, uxz), add2(Z, uxz)), mx2(add2(XZ, uxz), add2(MM, vxz))),   // :212-218
+             mx2(mx2(add2(Y, vxz), add2(XY, vxz)), add2(YZ, vxz)));
+  // M: every state plus the successor's triple score (src/PE_1cyc.v:162-170)
+  uint32_t s3;
+  if constexpr (SOP) s3 = pk_mad(eab, c.dmS, pk_mad(ebc, c.dmS, pk_mad(eac, c.dmS, c.mm3S)));
+  else s3 = pk_mad(eab, pk_mad(ebc, c.d1S, c.d0S), c.neS);
+  oM = mx2(mx2(mx2(add2(MM, s3), add2(X, s3)), mx2(add2(Y, s3), add2(Z, s3))),
+           mx2(mx2(add2(XY, s3), add2(YZ, s3)), add2(XZ, s3)));
+}
+
+// LDS: xr [NW-1][4][M][64][16] wave w -> w+1 records {Iy, Ixy, Iyz, M}
+//      xr0 [PD][M][64][16]     ring rows prefetched for wave 0 (LDS-DMA)
+//      sA2 [P+ZT] u32          A codes (1 << s) of positions k (lo) and k+64M (hi)
+//      sB  [LB+1] u32          B code, both halves
+//      fin [7][M][64] u32      the final cell's states (wave w_f)
+template <int M, bool SOP>
+__global__ __launch_bounds__(64 * LIT_NW) void literal_kernel(
+    const uint8_t *__restrict__ seqs, const int64_t *__restrict__ offs, int32_t n, int32_t P, int32_t R,
+    int32_t lds_a, int32_t lds_b, int64_t ring_stride, uint8_t *__restrict__ ring_base,
+    int32_t *__restrict__ scores, int32_t *__restrict__ final7, LitArgs ca) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int NW = LIT_NW, S = LIT_S, PD = LIT_PD, ZT = 128 * M;
+  constexpr int PAIR_BYTES = 64 * REC_BYTES, SLOT_BYTES = M * PAIR_BYTES;
+  uint8_t *xr = smem;
+  uint8_t *xr0 = xr + (NW - 1) * 4 * SLOT_BYTES;
+  uint32_t *sA2 = (uint32_t *)(xr0 + PD * SLOT_BYTES);
+  uint32_t *sB = (uint32_t *)((uint8_t *)sA2 + lds_a);
+  uint32_t *fin = (uint32_t *)((uint8_t *)sB + lds_b);
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t sel = lane == 0 ? 0x05040302u : 0x07060504u;  // zshift: lane 0 low half = the face
+  uint32_t ones = 0x00010001u, zero = 0u;
+  asm volatile("" : "+v"(ones), "+v"(zero));
+  const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
+                          4u * (uint32_t)(ZT - M * lane - (M - 1));
+  const int32_t lag = P - S * (NW - 1);
+
+  for (int tri = blockIdx.x; tri < n; tri += gridDim.x) {
+    const int64_t o0 = offs[3 * (int64_t)tri], o1 = offs[3 * (int64_t)tri + 1];
+    const int64_t o2 = offs[3 * (int64_t)tri + 2], o3 = offs[3 * (int64_t)tri + 3];
+    const int32_t la = (int32_t)(o1 - o0), lb = (int32_t)(o2 - o1), lc = (int32_t)(o3 - o2);
+    uint8_t *ring = ring_base + (int64_t)blockIdx.x * ring_stride;
+    auto sym = [&](int64_t base, int32_t i, int32_t len) -> uint32_t {
+      return (i >= 0 && i < len) ? 1u << tsa_sym(seqs, base + i, ca.packed) : 0u;
+    };
+    // ---- A codes of x' (lo: position k, hi: k + 64M) and B codes
+    for (int j = threadIdx.x; j < P + ZT; j += 64 * NW) {
+      const int x0 = ((j - ZT) % P + P) % P, x1 = ((j - ZT - 64 * M) % P + P) % P;
+      sA2[j] = sym(o0, x0, la) | (sym(o0, x1, la) << 16);
+    }
+    for (int i = threadIdx.x; i <= lb; i += 64 * NW) sB[i] = sym(o1, i, lb) * 0x00010001u;
+    __syncthreads();
+    // per-position c_{z+1} (successor) and the pushes of a zero cell
+    uint32_t cn[M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const int k0 = M * lane + i, k1 = 64 * M + k0;
+      cn[i] = sym(o2, k0 + 1, lc) | (sym(o2, k1 + 1, lc) << 16);
+    }
+    const uint32_t c1 = sym(o2, 0, lc), b1 = sB[0] & 0xFFFFu;
+    // A code of x' (0-based symbol index), 0 outside [0, la): the table's low half
+    auto acode = [&](int32_t xp) -> uint32_t { return (xp >= 0 && xp < la) ? sA2[xp + ZT] & 0xFFFFu : 0u; };
+    // a zero cell's pushes into successors with codes (an, bn, cn): per half
+    auto face_pair = [&](uint32_t p, uint32_t q) -> uint32_t {  // pair target, indicator per half
+      const uint32_t lo = (p & q & 0xFFFFu) ? ca.fP[1] : ca.fP[0];
+      const uint32_t hi = (p & q & 0xFFFF0000u) ? ca.fP[1] : ca.fP[0];
+      return (lo & 0xFFFFu) | (hi & 0xFFFF0000u);
+    };
+    auto face_m = [&](uint32_t an, uint32_t bn, uint32_t cc) -> uint32_t {
+      uint32_t r = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t m = 0xFFFFu << (16 * h);
+        const int idx = ((an & bn & m) ? 4 : 0) | ((bn & cc & m) ? 2 : 0) | ((an & cc & m) ? 1 : 0);
+        r |= ca.fM[idx] & m;
+      }
+      return r;
+    };
+    // ring rows of wave 0's first lap: row 0's pushes into row 1 at step
+    // t_r = (r + lag) mod R, where position k sits at x' = t_r - k
+    auto row0 = [&](int32_t t_r, int i, uint4 &rec) {
+      const int k0 = M * lane + i, k1 = 64 * M + k0;
+      const uint32_t an = acode(t_r - k0) | (acode(t_r - k1) << 16);
+      const uint32_t bb = b1 * 0x00010001u;
+      rec = make_uint4(ca.fS[1], face_pair(an, bb), face_pair(bb, cn[i]), face_m(an, bb, cn[i]));
+    };
+    for (int64_t j = threadIdx.x; j < (int64_t)R * M * 64; j += 64 * NW) {  // j % 64 == lane
+      const int32_t r = (int32_t)(j / (M * 64)), i = (int32_t)((j / 64) % M);
+      uint4 rec;
+      row0((r + lag) % R, i, rec);
+      ((uint4 *)ring)[j] = rec;
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    uint32_t bn[M], oIx[M], shIz[M], svIxy[M], svIyz[M], shIxz[2][M], svM[2][M];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      bn[i] = oIx[i] = shIz[i] = svIxy[i] = svIyz[i] = 0u;
+      shIxz[0][i] = shIxz[1][i] = svM[0][i] = svM[1][i] = 0u;
+    }
+    int32_t xpos0 = (P - ((S * w) % P)) % P;  // position at x' = 0 at step t
+    int32_t lap0 = w == 0 ? 0 : -1;
+    auto bcode = [&](int32_t row) -> uint32_t { return (row >= 0 && row < lb) ? sB[row] : 0u; };
+    uint32_t binj = bcode(lap0 * NW + w + 1);  // b_{y+1} of the row that starts at x' = 0
+    uint32_t bcur = bcode(lap0 * NW + w);      // b_y of position 0's row (the z = 0 face)
+    const int32_t lap_f = (lb - 1) / NW, w_f = (lb - 1) % NW, k_f = lc - 1;
+    const int32_t t_f = lap_f * P + la + S * w_f + k_f;  // cell (la, lb, lc) at x' = la
+    const int32_t T = t_f + 1;
+    if (w == 0) {
+#pragma unroll 1
+      for (int s = 0; s < PD; ++s) {
+        const int32_t row = ((s - lag) % R + R) % R;
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+          dma16(ring + ((int64_t)row * M + i) * PAIR_BYTES + lane * REC_BYTES,
+                xr0 + (s % PD) * SLOT_BYTES + i * PAIR_BYTES);
+      }
+    }
+    int32_t dma_row = ((PD - lag) % R + R) % R;
+    int32_t st_row = 0;
+    uint32_t a_nx[M];
+    load_a<M>(a_lane + 4u * (uint32_t)xpos0, a_nx);
+    // z = 0 face of position 0 (z = 1): a zero cell's pushes with its own
+    // symbols, uniform per wave: to Iz a constant, to Iyz by [b_y = c_1] (per
+    // row), to Ixz by [a_x = c_1] and to M by the three indicators
+    auto zfaces = [&](uint32_t &fz, uint32_t &fyz, uint32_t &fxz, uint32_t &fm) {
+      const uint32_t a2 = __builtin_amdgcn_readfirstlane(
+          *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t)(
+              (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 + 4u * (uint32_t)(xpos0 + ZT))) &
+          0xFFFFu;
+      const uint32_t by = bcur & 0xFFFFu;
+      fz = ca.fS[2];
+      fyz = ca.fP[(by & c1) ? 1 : 0];
+      fxz = ca.fP[(a2 & c1) ? 1 : 0];
+      fm = ca.fM[((a2 & by) ? 4 : 0) | ((by & c1) ? 2 : 0) | ((a2 & c1) ? 1 : 0)];
+    };
+
+    auto step = [&](auto ph, auto role, int32_t t) {
+      constexpr int Q = decltype(ph)::value;  // t & 3
+      constexpr int PH = Q & 1;
+      constexpr int ROLE = decltype(role)::value;
+      uint32_t a[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) a[i] = a_nx[i];
+      uint4 rec[M];
+      if constexpr (ROLE == 0) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(M * (PD - 1)) : "memory");
+        const uint8_t *src = xr0 + (t % PD) * SLOT_BYTES + lane * REC_BYTES;
+#pragma unroll
+        for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
+      } else {
+        const uint8_t *src = xr + ((w - 1) * 4 + ((Q + 2) & 3)) * SLOT_BYTES + lane * REC_BYTES;
+#pragma unroll
+        for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
+      }
+      uint32_t X[M], Y[M], Z[M], XY[M], YZ[M], XZ[M], MM[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        X[i] = oIx[i];
+        Y[i] = rec[i].x;
+        Z[i] = shIz[i];
+        XY[i] = svIxy[i];
+        YZ[i] = svIyz[i];
+        XZ[i] = shIxz[PH][i];
+        MM[i] = svM[PH][i];
+      }
+      // ---- x' = 0 at position xpos0: the face column (all 7 inputs 0) and the
+      // next row's B code for its successors
+      if (xpos0 < ZT) {
+        int32_t ls, is, hs;
+        pos_split<M>(xpos0, ls, is, hs);
+        const uint32_t hm = hs ? 0xFFFF0000u : 0x0000FFFFu;
+        uint32_t m1;
+        asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(m1) : "v"(hm), "s"(1ull << ls));
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          if (i == is) {
+            X[i] = vbfi(m1, zero, X[i]);
+            Y[i] = vbfi(m1, zero, Y[i]);
+            Z[i] = vbfi(m1, zero, Z[i]);
+            XY[i] = vbfi(m1, zero, XY[i]);
+            YZ[i] = vbfi(m1, zero, YZ[i]);
+            XZ[i] = vbfi(m1, zero, XZ[i]);
+            MM[i] = vbfi(m1, zero, MM[i]);
+            bn[i] = vbfi(m1, binj, bn[i]);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < M; ++i) asm volatile("" : "+v"(bn[i]));
+      // the final cell's states (src/TriAlign_1cyc.v:130,138,141-142)
+      if (t == t_f && w == w_f) {
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          fin[(0 * M + i) * 64 + lane] = MM[i];
+          fin[(1 * M + i) * 64 + lane] = X[i];
+          fin[(2 * M + i) * 64 + lane] = Y[i];
+          fin[(3 * M + i) * 64 + lane] = Z[i];
+          fin[(4 * M + i) * 64 + lane] = XY[i];
+          fin[(5 * M + i) * 64 + lane] = YZ[i];
+          fin[(6 * M + i) * 64 + lane] = XZ[i];
+        }
+      }
+      uint32_t nIx[M], oIy[M], oIz[M], oIxy[M], oIyz[M], oIxz[M], oM[M];
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < M; ++i)
+        push_literal<SOP>(ca, ones, MM[i], X[i], Y[i], Z[i], XY[i], YZ[i], XZ[i], a[i], bn[i], cn[i], nIx[i],
+                          oIy[i], oIz[i], oIxy[i], oIyz[i], oIxz[i], oM[i]);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      // ---- records: to the wave below, or (last wave) the ring
+      if constexpr (ROLE != 2) {
+        uint8_t *dst = xr + (w * 4 + Q) * SLOT_BYTES + lane * REC_BYTES;
+#pragma unroll
+        for (int i = 0; i < M; ++i) lds_write16(dst + i * PAIR_BYTES, make_uint4(oIy[i], oIxy[i], oIyz[i], oM[i]));
+      } else {
+        if (t < ZT + S * NW) {  // not-started positions: row 0's pushes (wave 0 meets them at t + lag)
+          const int32_t lim = t - S * w;
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            const uint32_t m = ((M * lane + i > lim) ? 0x0000FFFFu : 0u) |
+                               ((64 * M + M * lane + i > lim) ? 0xFFFF0000u : 0u);
+            uint4 f;
+            row0(t + lag, i, f);
+            oIy[i] = bfi(m, f.x, oIy[i]);
+            oIxy[i] = bfi(m, f.y, oIxy[i]);
+            oIyz[i] = bfi(m, f.z, oIyz[i]);
+            oM[i] = bfi(m, f.w, oM[i]);
+          }
+        }
+        uint4 *dst = (uint4 *)__builtin_assume_aligned(ring + (int64_t)st_row * SLOT_BYTES + lane * REC_BYTES, 16);
+#pragma unroll
+        for (int i = 0; i < M; ++i) dst[i * 64] = make_uint4(oIy[i], oIxy[i], oIyz[i], oM[i]);
+      }
+      // ---- advance: position 0 moves on (a wrap starts a new row), then the shifts
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        oIx[i] = nIx[i];
+        svIxy[i] = rec[i].y;
+      }
+      if (++xpos0 == P) {
+        xpos0 = 0;
+        ++lap0;
+        binj = bcode(lap0 * NW + w + 1);
+        bcur = bcode(lap0 * NW + w);
+      }
+      uint32_t fz, fyz, fxz, fm;
+      zfaces(fz, fyz, fxz, fm);
+      uint32_t rz[M], rw[M];
+#pragma unroll
+      for (int i = 0; i < M; ++i) { rz[i] = rec[i].z; rw[i] = rec[i].w; }
+      zshift<M>(shIxz[PH], oIxz, sel, fxz);  // (the faces sit in both halves)
+      zshift<M>(shIz, oIz, sel, fz);
+      zshift<M>(svIyz, rz, sel, fyz);
+      zshift<M>(svM[PH], rw, sel, fm);
+      load_a<M>(a_lane + 4u * (uint32_t)xpos0, a_nx);
+      if constexpr (ROLE == 0) {
+#pragma unroll
+        for (int i = 0; i < M; ++i)
+          dma16(ring + ((int64_t)dma_row * M + i) * PAIR_BYTES + lane * REC_BYTES,
+                xr0 + (t % PD) * SLOT_BYTES + i * PAIR_BYTES);
+        if (++dma_row == R) dma_row = 0;
+      }
+      if constexpr (ROLE == 2) {
+        if (++st_row == R) st_row = 0;
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(M * 4) : "memory");
+      }
+      if constexpr (PH == 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    auto run = [&](auto role) {
+      constexpr std::integral_constant<int, 0> Q0{};
+      constexpr std::integral_constant<int, 1> Q1{};
+      constexpr std::integral_constant<int, 2> Q2{};
+      constexpr std::integral_constant<int, 3> Q3{};
+#pragma unroll 1
+      for (int32_t t = 0; t < T; t += 4) {  // whole groups of four (past T: harmless cells)
+        step(Q0, role, t);
+        step(Q1, role, t + 1);
+        step(Q2, role, t + 2);
+        step(Q3, role, t + 3);
+      }
+    };
+    if (w == 0) run(std::integral_constant<int, 0>{});
+    else if (w == NW - 1) run(std::integral_constant<int, 2>{});
+    else run(std::integral_constant<int, 1>{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x < 7) {  // unshift the final cell's states
+      int32_t l_f, i_f, h_f;
+      pos_split<M>(k_f, l_f, i_f, h_f);
+      const uint32_t v = fin[(threadIdx.x * M + i_f) * 64 + l_f];
+      const int32_t s = (int32_t)(int16_t)(uint16_t)(h_f ? (v >> 16) : (v & 0xFFFF)) >> ca.sh;
+      fin[7 * M * 64 + threadIdx.x] = (uint32_t)s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int32_t best = (int32_t)fin[7 * M * 64];
+#pragma unroll
+      for (int s = 1; s < 7; ++s) best = max(best, (int32_t)fin[7 * M * 64 + s]);
+      scores[tri] = best;  // FINAL MAX7, src/TriAlign_1cyc.v:141-142
+      if (final7)
+        for (int s = 0; s < 7; ++s) final7[7 * (int64_t)tri + s] = (int32_t)fin[7 * M * 64 + s];
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+static inline int32_t wrap_bits(int64_t v, int bits) {
+  const uint64_t u = (uint64_t)v << (64 - bits);
+  return (int32_t)((int64_t)u >> (64 - bits));
+}
+static LitArgs lit_args(const KParams &kp) {
+  LitArgs c;
+  memset(&c, 0, sizeof(c));
+  const int bits = kp.bits ? kp.bits : 16;
+  const int sh = 16 - bits;
+  c.sh = sh;
+  c.packed = kp.packed;
+  auto S = [&](int64_t v) { return ((uint32_t)(uint16_t)(uint32_t)(wrap_bits(v, bits) << sh)) * 0x00010001u; };
+  const int32_t GE = kp.pen[SIXY][SIX], GO = kp.pen[SIXY][SM];
+  c.n2E = S(-2 * GE);
+  c.nOE = S(-(GO + GE));
+  c.n2O = S(-2 * GO);
+  c.dmS = S((int64_t)kp.match - kp.mismatch);
+  c.mmE = S((int64_t)kp.mismatch - GE);
+  c.nDOE = S(-(GO - GE));
+  c.d1S = S((int64_t)kp.s3_eq - kp.s3_ab);
+  c.d0S = S((int64_t)kp.s3_ab - kp.s3_ne);
+  c.neS = S(kp.s3_ne);
+  c.mm3S = S(3LL * kp.mismatch);
+  // a zero cell's pushes: the literal MAX7 of wrapped candidates 0 - P + add
+  auto push0 = [&](int T, int64_t add) {
+    int32_t m = INT32_MIN;
+    for (int s = 0; s < 7; ++s) m = std::max(m, wrap_bits((int64_t)-kp.pen[T][s] + add, bits));
+    return S(m);
+  };
+  c.fS[0] = push0(SIX, 0);
+  c.fS[1] = push0(SIY, 0);
+  c.fS[2] = push0(SIZ, 0);
+  c.fP[0] = push0(SIXY, kp.mismatch);
+  c.fP[1] = push0(SIXY, kp.match);
+  for (int idx = 0; idx < 8; ++idx) {
+    const bool eab = idx & 4, ebc = idx & 2, eac = idx & 1;
+    int64_t s3;
+    if (kp.s3_mode == TSA_S3_SOP)
+      s3 = (eab ? kp.match : kp.mismatch) + (int64_t)(ebc ? kp.match : kp.mismatch) + (eac ? kp.match : kp.mismatch);
+    else
+      s3 = eab ? (ebc ? kp.s3_eq : kp.s3_ab) : kp.s3_ne;
+    c.fM[idx] = push0(SM, wrap_bits(s3, bits));
+  }
+  return c;
+}
+
+template <int M, bool SOP>
+static int launch_lit(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, int32_t max_lb,
+                      const LitGeom &g, int32_t *d_scores, int32_t *d_final7, void *d_ws, const LitArgs &ca,
+                      hipStream_t stream) {
+  const int32_t lds_a = 4 * (g.P + 128 * M), lds_b = 4 * ((max_lb + 4) & ~3);
+  auto kfn = literal_kernel<M, SOP>;
+  if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds) != hipSuccess)
+    return TSA_EDEVICE;
+  const int grid = n < 65535 ? n : 65535;
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * LIT_NW), g.lds, stream, d_seqs, d_offsets, n, g.P, g.R, lds_a,
+                     lds_b, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, d_final7, ca);
+  return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
+}
+
+int literal_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, int32_t max_la,
+                         int32_t max_lb, int32_t max_lc, const KParams &kp, int32_t *d_scores,
+                         int32_t *d_final7, void *d_ws, size_t ws_bytes, hipStream_t stream) {
+  if (n <= 0) return TSA_OK;
+  if (!literal_shape_ok(max_la, max_lb, max_lc)) return TSA_EINVAL;
+  if (ws_bytes < literal_workspace_bytes(n, max_la, max_lb, max_lc)) return TSA_ENOMEM;
+  const LitGeom g = lit_geom(max_la, max_lb, max_lc);
+  const LitArgs ca = lit_args(kp);
+  const bool sop = kp.s3_mode == TSA_S3_SOP;
+  if (g.M == 1)
+    return sop ? launch_lit<1, true>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_final7, d_ws, ca, stream)
+               : launch_lit<1, false>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_final7, d_ws, ca, stream);
+  return sop ? launch_lit<2, true>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_final7, d_ws, ca, stream)
+             : launch_lit<2, false>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_final7, d_ws, ca, stream);
+}
+
+}  // namespace tsa

@@ -259,7 +259,9 @@ static int upgrade_checked(int kind, int32_t kernel, int32_t n, const tsa_params
 // error word and rescore with LAP_OFF; the async path keeps LAP_RESIDENT
 static size_t workspace_for(int kind, int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
                             const tsa_params *p, LapPolicy lap = LAP_RESIDENT) {
-  if (kind == TSA_KERNEL_PLANE) return plane_workspace_bytes(n, max_la, max_lb, max_lc);
+  if (kind == TSA_KERNEL_PLANE)
+    return literal_helix_chosen(n, max_la, max_lb, max_lc) ? literal_workspace_bytes(n, max_la, max_lb, max_lc)
+                                                           : plane_workspace_bytes(n, max_la, max_lb, max_lc);
   KParams kp;
   if (build_kparams(p, &kp)) return 0;
   return pencil_workspace_bytes(n, max_la, max_lb, max_lc, kp, value_bound(p, max_la, max_lb, max_lc),
@@ -276,14 +278,19 @@ static int launch_kind(int kind, const uint8_t *d_seqs, const int64_t *d_off, in
                        int32_t max_la, int32_t max_lb, int32_t max_lc, const tsa_params *p,
                        int32_t *d_scores, int32_t *d_final7, void *ws, size_t ws_bytes,
                        hipStream_t s, LapPolicy lap = LAP_RESIDENT, int32_t **d_err = nullptr,
-                       int32_t packed = 0) {
+                       int32_t packed = 0, int32_t choice_n = -1) {
+  // choice_n: the batch size the workspace was sized for (a chunk may be
+  // smaller, and must run the kernel that workspace was sized for)
   KParams kp;
   int rc = build_kparams(p, &kp);
   if (rc) return rc;
   kp.packed = packed;
   if (kind == TSA_KERNEL_PLANE)
-    return plane_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp, d_scores, d_final7,
-                              ws, ws_bytes, s);
+    return literal_helix_chosen(choice_n < 0 ? n : choice_n, max_la, max_lb, max_lc)
+               ? literal_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp, d_scores, d_final7, ws,
+                                      ws_bytes, s)
+               : plane_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp, d_scores, d_final7,
+                                    ws, ws_bytes, s);
   const CheckLimits lim = check_limits(p);
   return pencil_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp,
                              value_bound(p, max_la, max_lb, max_lc), d_scores, ws, ws_bytes, s,
@@ -353,7 +360,7 @@ static int run_host_batch_on_device(int device, const uint8_t *seqs, const int64
     int32_t *d_err = nullptr;
     rc = launch_kind(kind, d_seqs, d_off + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p,
                      d_scores + c0, d_final ? d_final + 7 * (int64_t)c0 : nullptr, d_ws,
-                     ws_bytes, s, LAP_STREAM, &d_err);
+                     ws_bytes, s, LAP_STREAM, &d_err, 0, chunk);
     if (rc == TSA_OK && kind == TSA_KERNEL_CHECKED) {
       // certified scores stand; a chunk with any other (uncertified, or a
       // timed-out hand-off) is rescored by the literal PLANE kernel
@@ -368,7 +375,7 @@ static int run_host_batch_on_device(int device, const uint8_t *seqs, const int64
         g_check_fallbacks.fetch_add(herr ? cn : bad);
         if (herr) g_lap_fallbacks.fetch_add(1);
         rc = launch_kind(TSA_KERNEL_PLANE, d_seqs, d_off + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc,
-                         p, d_scores + c0, nullptr, d_ws, ws_bytes, s);
+                         p, d_scores + c0, nullptr, d_ws, ws_bytes, s, LAP_RESIDENT, nullptr, 0, chunk);
       }
     } else if (rc == TSA_OK && d_err) {  // lap kernel: a timed-out hand-off invalidates the chunk
       int32_t herr = 0;
@@ -656,7 +663,8 @@ int tsa_describe_plan(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
   if (kind < 0) return TSA_ERANGE;
   if (sync) kind = upgrade_checked(kind, kernel, n, p, max_la, max_lb, max_lc);
   if (kind == TSA_KERNEL_PLANE) {
-    snprintf(buf, len, "plane");
+    snprintf(buf, len, literal_helix_chosen(std::min(n, 65535), max_la, max_lb, max_lc) ? "plane literal-helix"
+                                                                                         : "plane");
     return TSA_OK;
   }
   const LapPolicy lap = sync ? LAP_STREAM : LAP_RESIDENT;
@@ -703,9 +711,9 @@ static int score_batch_async(const uint8_t *d_seqs, const int64_t *d_offsets, in
   hipStream_t s = (hipStream_t)stream;
   for (int32_t c0 = 0; c0 < n; c0 += 65535) {
     const int32_t cn = std::min<int32_t>(65535, n - c0);
-    const size_t wsz = workspace_for(kind, cn, max_la, max_lb, max_lc, p);
     int rc = launch_kind(kind, d_seqs, d_offsets + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p,
-                         d_scores + c0, nullptr, d_workspace, wsz, s, LAP_RESIDENT, nullptr, packed);
+                         d_scores + c0, nullptr, d_workspace, workspace_bytes, s, LAP_RESIDENT, nullptr, packed,
+                         std::min<int32_t>(n, 65535));
     if (rc) return rc;
   }
   return TSA_OK;

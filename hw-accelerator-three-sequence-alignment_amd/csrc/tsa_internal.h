@@ -64,6 +64,18 @@ int plane_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t 
                        int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
                        int32_t *d_scores, int32_t *d_final7, void *d_ws, size_t ws_bytes,
                        hipStream_t stream, uint32_t *d_tb = nullptr);
+// ---- literal helix (literal_kernel.hip): TSA_KERNEL_PLANE's batch path -----
+// The RTL's literal arithmetic in push form on the helix schedule, LC <= 256.
+bool literal_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc);
+size_t literal_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc);
+int literal_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, int32_t max_la,
+                         int32_t max_lb, int32_t max_lc, const KParams &kp, int32_t *d_scores,
+                         int32_t *d_final7, void *d_ws, size_t ws_bytes, hipStream_t stream);
+// Which literal kernel a batch runs: the literal helix (batches the helix
+// shape holds) or the plane sweep (single cubes, LC > 256, traceback).
+// TSA_PENCIL_MODE=plane / =literal force one (tests).
+bool literal_helix_chosen(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc);
+
 // Traceback: pointer cube of one (la,lb,lc) triple and the walk kernel.
 size_t tb_cube_bytes(int32_t la, int32_t lb, int32_t lc);
 __global__ void tb_walk(const uint32_t *tb, const int32_t *final7, int32_t la, int32_t lb,

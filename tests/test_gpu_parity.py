@@ -675,3 +675,54 @@ def test_split_cube_across_devices(gpu, orc, synth, devs):
     b, c = b[:173], c[:131]
     assert gpu.score_multi(a, b, c, devs)[0] == orc.score(a, b, c)
     assert (gpu.fallback_count(), gpu.check_fallback_count()) == before
+
+
+# ---- the literal helix (csrc/literal_kernel.hip): TSA_KERNEL_PLANE's batch path
+@pytest.mark.parametrize("bits,s3_mode", [(12, 0), (12, 1), (9, 0), (6, 1), (4, 0), (16, 0)])
+def test_literal_helix_matches_oracle(gpu, orc, monkeypatch, bits, s3_mode):
+    """The RTL's literal arithmetic in push form on the helix schedule (every
+    candidate wrapped to SCORE_BITS by int16 arithmetic on values shifted left
+    by 16 - SCORE_BITS; tools/literal_emu.py replays it): narrow words that
+    wrap, both s3 modes, ragged batches over M = 1 and 2, related triples."""
+    monkeypatch.setenv("TSA_PENCIL_MODE", "literal")
+    rng = np.random.default_rng(200 + bits + s3_mode)
+    p, op = gpu.TsaParams.default(score_bits=bits, s3_mode=s3_mode), orc.default_params(score_bits=bits, s3_mode=s3_mode)
+    for n, hi in ((7, (150, 30, 100)), (5, (260, 21, 256)), (3, (40, 17, 129))):
+        triples = [tuple(rng.integers(0, 5, int(rng.integers(1, h + 1))).astype(np.uint8) for h in hi)
+                   for _ in range(n)]
+        a = rng.integers(0, 4, 120).astype(np.uint8)
+        triples.append((a, a[:60].copy(), a[:110].copy()))  # related: high scores
+        ml = [max(len(t[k]) for t in triples) for k in range(3)]
+        assert gpu.describe_plan(len(triples), *ml, p, kernel="plane") == "plane literal-helix"
+        seqs, offs = gpu.pack_batch(triples)
+        ws = gpu.workspace_size(len(triples), *ml, p, "plane")
+        import torch
+        d_seqs, d_offs = torch.from_numpy(seqs).cuda(), torch.from_numpy(offs).cuda()
+        d_sc = torch.zeros(len(triples), dtype=torch.int32, device="cuda")
+        d_ws = torch.empty(max(ws, 16), dtype=torch.uint8, device="cuda")
+        gpu.score_batch_async(d_seqs.data_ptr(), d_offs.data_ptr(), len(triples), *ml, d_sc.data_ptr(),
+                              d_ws.data_ptr(), ws, torch.cuda.current_stream().cuda_stream, p, "plane")
+        torch.cuda.synchronize()
+        got = d_sc.cpu().numpy()
+        assert np.array_equal(got, orc.score_batch(seqs, offs, op, nthreads=8)), (bits, s3_mode, ml)
+
+
+def test_literal_helix_final_states_and_wrap(gpu, orc, golden, monkeypatch):
+    """Final 7-tuples from the literal helix (the 84-bit SRAM word,
+    src/TriAlign_1cyc.v:130,138) on the golden fixtures, and an all-match cube
+    whose diagonal wraps a 9-bit word (3 x 120 = 360 > 255)."""
+    monkeypatch.setenv("TSA_PENCIL_MODE", "literal")
+    used = 0
+    for c in golden:
+        if len(c["c"]) > 256 or "final7" not in c:
+            continue
+        p = gpu.TsaParams.default(**c["params"])
+        s, fin = gpu.score(c["a"], c["b"], c["c"], p, final_states=True)
+        assert (s, list(fin)) == (c["score"], c["final7"]), c["name"]
+        used += 1
+    assert used >= 10
+    a = np.zeros(120, np.uint8)
+    p9, o9 = gpu.TsaParams.default(score_bits=9), orc.default_params(score_bits=9)
+    ref = orc.score(a, a, a, o9, final_states=True)
+    s, fin = gpu.score(a, a, a, p9, final_states=True)
+    assert (s, tuple(fin)) == ref and ref[0] != 360

@@ -44,3 +44,18 @@ def test_emulated_vspace_lam2(orc):
     a, b, c = (rng.integers(0, 4, n) for n in (50, 11, 90))
     p = orc.default_params(score_bits=0, match=2, mismatch=-2, gap_open=3, gap_extend=2)
     assert pencil_emu.emulate([(a, b, c)], vs=True, **kw) == [orc.score(a, b, c, p)]
+
+
+@pytest.mark.parametrize("la,lb,lc,sop,bits", [(8, 8, 8, 0, 12), (20, 9, 30, 0, 12), (47, 17, 128, 1, 12),
+                                               (60, 3, 130, 0, 12), (30, 20, 40, 0, 5), (25, 17, 33, 1, 4)])
+def test_emulated_literal_helix(orc, la, lb, lc, sop, bits):
+    """tools/literal_emu.py: the literal push form on the helix schedule (the
+    x = 0 face column, row 0's pushes in the ring, the z = 0 pushes of a zero
+    cell with position 0's own symbols) equals the literal oracle, final
+    7-tuple included, also for words narrow enough to wrap."""
+    import literal_emu
+    rng = np.random.default_rng(la * 1000 + lb * 10 + lc)
+    a, b, c = (rng.integers(0, 5, n) for n in (la, lb, lc))
+    s, fin = literal_emu.emulate(a, b, c, sop=bool(sop), bits=bits)
+    assert (s, tuple(fin)) == orc.score(a, b, c, orc.default_params(s3_mode=sop, score_bits=bits),
+                                        final_states=True)
