@@ -214,6 +214,16 @@ __global__ __launch_bounds__(64 * LIT_NW) void literal_kernel(
       bn[i] = oIx[i] = shIz[i] = svIxy[i] = svIyz[i] = 0u;
       shIxz[0][i] = shIxz[1][i] = svM[0][i] = svM[1][i] = 0u;
     }
+    if (w == 0) {  // position 0 at x' = 1 in step 1: its z = 0 faces, as if shifted in at step -1
+      const uint32_t a0 = acode(0);
+      const uint32_t fxz = ca.fP[(a0 & c1) ? 1 : 0];
+      const uint32_t fm = ca.fM[((a0 & b1) ? 4 : 0) | ((b1 & c1) ? 2 : 0) | ((a0 & c1) ? 1 : 0)];
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        shIxz[1][i] = fxz;
+        svM[1][i] = fm;
+      }
+    }
     int32_t xpos0 = (P - ((S * w) % P)) % P;  // position at x' = 0 at step t
     int32_t lap0 = w == 0 ? 0 : -1;
     auto bcode = [&](int32_t row) -> uint32_t { return (row >= 0 && row < lb) ? sB[row] : 0u; };

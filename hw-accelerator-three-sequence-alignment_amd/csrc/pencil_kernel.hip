@@ -368,6 +368,13 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       // the step-0 injection's (0, y-1, z-1) face is H(0) - lam (wave 0 starts
       // its first row at step 0 with no wrap that would have set it)
       Hr[3] = U(H(Hr[0]) - H(pa.v_lam));
+      if (w == 0) {  // position 0's z = 0 faces at steps 0 and 1 (as if shifted in at steps -1, -2)
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          shIz[i] = svIyz[i] = svM[1][i] = Hr[0];
+          shIxz[1][i] = Hr[1];
+        }
+      }
     }
     // wave 0: prime the LDS-DMA pipeline (ring row of step s = s - P + NW - 1)
     if (w == 0) {

@@ -180,6 +180,17 @@ def test_vspace_helix(gpu, orc, monkeypatch, s3_mode):
             seqs, offs = gpu.pack_batch(triples)
             got = gpu.score_batch(triples, p)
             assert np.array_equal(got, orc.score_batch(seqs, offs, op, nthreads=8)), (kw, ml)
+    # related and homopolymer triples: the optimum may leave the z = 0 face at
+    # the first steps (position 0's initial faces)
+    p = gpu.TsaParams.default(s3_mode=s3_mode)
+    triples = []
+    for _ in range(40):
+        L = int(rng.integers(2, 40))
+        a = rng.integers(0, 4, L).astype(np.uint8)
+        triples.append((a, a[: int(rng.integers(1, L + 1))].copy(), a[: int(rng.integers(1, L + 1))].copy()))
+    seqs, offs = gpu.pack_batch(triples)
+    assert np.array_equal(gpu.score_batch(triples, p),
+                          orc.score_batch(seqs, offs, orc.default_params(s3_mode=s3_mode), nthreads=8))
     # all-match (the V-space bound's top) and all-distinct triples
     p = gpu.TsaParams.default()
     for a, b, c in ((np.zeros(256, np.uint8),) * 3, tuple(np.full(200, v, np.uint8) for v in (0, 1, 2))):
@@ -692,6 +703,10 @@ def test_literal_helix_matches_oracle(gpu, orc, monkeypatch, bits, s3_mode):
                    for _ in range(n)]
         a = rng.integers(0, 4, 120).astype(np.uint8)
         triples.append((a, a[:60].copy(), a[:110].copy()))  # related: high scores
+        for _ in range(12):  # short related / homopolymer triples
+            L = int(rng.integers(2, 30))
+            h = rng.integers(0, 4, L).astype(np.uint8)
+            triples.append((h, h[: int(rng.integers(1, L + 1))].copy(), h[: int(rng.integers(1, L + 1))].copy()))
         ml = [max(len(t[k]) for t in triples) for k in range(3)]
         assert gpu.describe_plan(len(triples), *ml, p, kernel="plane") == "plane literal-helix"
         seqs, offs = gpu.pack_batch(triples)

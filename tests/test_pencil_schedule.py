@@ -59,3 +59,17 @@ def test_emulated_literal_helix(orc, la, lb, lc, sop, bits):
     s, fin = literal_emu.emulate(a, b, c, sop=bool(sop), bits=bits)
     assert (s, tuple(fin)) == orc.score(a, b, c, orc.default_params(s3_mode=sop, score_bits=bits),
                                         final_states=True)
+
+
+def test_emulated_related_triples(orc):
+    """Related and homopolymer triples (long matching runs: the optimum leaves
+    the z = 0 face at the very first steps) in the V-space and literal forms."""
+    import literal_emu
+    import pencil_emu
+    rng = np.random.default_rng(1)
+    for _ in range(60):
+        L = int(rng.integers(2, 20))
+        a = rng.integers(0, 4, L).astype(np.uint8)
+        t = (a, a[: int(rng.integers(1, L + 1))].copy(), a[: int(rng.integers(1, L + 1))].copy())
+        assert pencil_emu.emulate([t], vs=True) == [orc.score(*t, orc.default_params(score_bits=0))], t
+        assert literal_emu.emulate(*t)[0] == orc.score(*t), t

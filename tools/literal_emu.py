@@ -106,6 +106,11 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, bits=12):
                        svIxy=np.zeros(shape, np.int64), svIyz=np.zeros(shape, np.int64),
                        shIxz=[np.zeros(shape, np.int64)] * 2, svM=[np.zeros(shape, np.int64)] * 2,
                        bn=np.full(shape, -1), xpos0=(P - (S * w) % P) % P, lap0=0 if w == 0 else -1))
+    # wave 0, position 0 at x' = 1 in step 1: its z = 0 faces (x - 1, y, 0) and
+    # (x - 1, y - 1, 0) would have been shifted in at step -1
+    f = push(zero7, np.full(shape, int(code(a, np.array(0)))), np.full(shape, int(B0)), np.full(shape, c1))
+    st[0]["shIxz"][1] = np.full(shape, int(f[6][0, 0, 0]))
+    st[0]["svM"][1] = np.full(shape, int(f[0][0, 0, 0]))
     lap_f, w_f, k_f = (lb - 1) // NW, (lb - 1) % NW, lc - 1
     t_f = lap_f * P + la + S * w_f + k_f          # x' = la at u = la
     fin = None

@@ -103,6 +103,10 @@ def emulate(triples, match=1, mismatch=-1, go=2, ge=1, sop=False, vs=False):
                 lp = u // P
                 return lam * (lp * NW + w + 1 + (u - lp * P))
             d["H"] = {0: h_at(0), 1: h_at(1), -1: h_at(0) - lam}
+            if w == 0:  # position 0's z = 0 faces at steps 0 and 1 ("shifted in" at steps -1, -2)
+                d["shIz"][:] = d["svIyz"][:] = d["H"][0]
+                d["shIxz"][1][:] = d["H"][1]
+                d["svM"][1][:] = d["H"][0]
         st.append(d)
 
     def shift(v, face):
