@@ -13,6 +13,10 @@ CLI      := $(PKG)/bin/tsa
 SRCS     := $(wildcard $(PKG)/csrc/*.hip)
 HDRS     := $(wildcard $(PKG)/csrc/*.h) include/trialign.h
 OBJS     := $(patsubst $(PKG)/csrc/%.hip,$(PKG)/build/%.o,$(SRCS))
+# host-only table of every kernel's SGPR/VGPR/scratch counts, generated from
+# the code objects (tools/kernel_meta.py; the lap grid's residency uses it)
+META_CPP := $(PKG)/build/kernel_meta.cpp
+META_OBJ := $(PKG)/build/kernel_meta.o
 
 ORACLE_SO  := oracle/_build/libtsa_oracle.so
 ORACLE_CLI := oracle/_build/tsa_oracle_cli
@@ -28,9 +32,15 @@ $(PKG)/build/%.o: $(PKG)/csrc/%.hip $(HDRS)
 $(PKG)/build/trialign_api.o: $(SRCS) $(PKG)/srchash.py
 $(PKG)/build/trialign_api.o: HIPFLAGS += -DTSA_SRC_HASH='"$(SRC_HASH)"'
 
-$(LIB): $(OBJS)
+$(META_CPP): $(OBJS) $(PKG)/tools/kernel_meta.py
+	python3 $(PKG)/tools/kernel_meta.py --cpp $@ $(OBJS)
+
+$(META_OBJ): $(META_CPP) $(PKG)/csrc/kernel_meta.h
+	g++ -O2 -std=c++17 -Wall -fPIC -I$(PKG)/csrc -c $< -o $@
+
+$(LIB): $(OBJS) $(META_OBJ)
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) -lpthread
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS) $(META_OBJ) -lpthread
 
 $(CLI): $(PKG)/tools/tsa_cli.cpp $(LIB) include/trialign.h
 	@mkdir -p $(dir $@)

@@ -57,6 +57,7 @@
 
 #include "pencil_common.h"
 #include "lap_kernel.h"
+#include "kernel_meta.h"
 
 namespace tsa {
 
@@ -1001,17 +1002,30 @@ static DevInfo dev_info() {
   return cache[d];
 }
 
+// The SGPR bound on lap workgroups per CU: waves per SIMD the SGPR file admits
+// (build-time kernel table, kernel_meta.h), a workgroup of NW + 1 waves taking
+// up to ceil((NW + 1) / 4) of them on one SIMD -- the margin the guide asks for
+// near the occupancy API's SGPR edge (MI355X_MICROARCH.md:463).
+int lap_sgpr_blocks_per_cu(int M, int NW, bool f16, bool sop) {
+  char prefix[64];
+  snprintf(prefix, sizeof prefix, "_ZN3tsa10lap_kernelILi%dELi%dELb%dELb%dELb0E", M, NW, f16 ? 1 : 0,
+           sop ? 1 : 0);
+  const int sgpr = kernel_sgpr_max(prefix);
+  return sgpr_waves_per_simd(sgpr < 0 ? 112 : sgpr) / ((NW + 1 + 3) / 4);
+}
 // Workgroups of one instantiation a CU holds, from the HIP occupancy API on the
-// real kernel (VGPRs, LDS); without a device, the LDS / wave-slot model.
+// real kernel (VGPRs, LDS) capped by the SGPR bound (the API reads one block
+// high at 81-112 SGPRs); without a device, the LDS / wave-slot model.
 template <int M, int NW, bool F16, bool SOP>
 static int lap_blocks_per_cu_t(size_t lds) {
   int nb = 0;
   int dev = -1;
+  const int sg = lap_sgpr_blocks_per_cu(M, NW, F16, SOP);
   if (hipGetDevice(&dev) == hipSuccess &&
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lap_kernel<M, NW, F16, SOP, false>, 64 * (NW + 1),
                                                    lds) == hipSuccess)
-    return nb;
-  return (int)std::min<size_t>(LDS_MAX / std::max<size_t>(lds, 1), 32 / (NW + 1));
+    return std::min(nb, sg);
+  return (int)std::min<size_t>(std::min<size_t>(LDS_MAX / std::max<size_t>(lds, 1), 32 / (NW + 1)), sg);
 }
 #define TSA_LAP_SHAPES(FN, M_, NW_, F16_, SOP_, ...)                                          \
   ((M_) == 1 ? ((NW_) == 4 ? TSA_ARITH(FN, 1, 4, F16_, SOP_, __VA_ARGS__)                      \

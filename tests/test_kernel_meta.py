@@ -1,0 +1,73 @@
+"""Kernel resources from the gfx950 code objects (tools/kernel_meta.py), no
+GPU needed: no kernel of the product path uses scratch (a private segment
+means a spilled or dynamically indexed register array), and the lap grid's
+residency is capped by the SGPR bound where the occupancy API reads one
+workgroup per CU high (MI355X_MICROARCH.md:463)."""
+import ctypes
+import glob
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+from conftest import PKG_DIR
+
+sys.path.insert(0, os.path.join(PKG_DIR, "tools"))
+
+
+@pytest.fixture(scope="module")
+def meta(tsa):
+    import kernel_meta
+    objs = sorted(glob.glob(os.path.join(PKG_DIR, "build", "*.o")))
+    objs = [o for o in objs if not o.endswith("kernel_meta.o")]
+    if not objs:
+        pytest.skip("no build objects (prebuilt library only)")
+    return kernel_meta.object_meta_all(objs)
+
+
+def test_every_kernel_is_listed(meta):
+    names = " ".join(meta)
+    for k in ("pencil_kernel", "lap_kernel", "literal_kernel", "plane_step_kernel", "tb_walk", "lap_certify"):
+        assert k in names, k
+
+
+def test_no_scratch_outside_the_widest_helix(meta):
+    """Only the M = 8 helix (LC 513..1024, 4 f16/int16 pairs x 8 registers x 7
+    states) runs out of the 256 VGPRs a 512-thread workgroup allows; every
+    other kernel, the literal helix and the lap kernel included, keeps its
+    registers in registers."""
+    scratch = {k: v["scratch"] for k, v in meta.items() if v.get("scratch", 0)}
+    for k in scratch:
+        assert k.startswith("_ZN3tsa13pencil_kernelILi8E"), (k, scratch[k])
+    assert all(s <= 512 for s in scratch.values())
+
+
+def test_generated_table_matches_objects(meta):
+    cpp = os.path.join(PKG_DIR, "build", "kernel_meta.cpp")
+    rows = dict((m.group(1), int(m.group(2))) for m in re.finditer(r'\{"([^"]+)", (\d+),', open(cpp).read()))
+    assert rows == {k: v["sgpr"] for k, v in meta.items()}
+
+
+def sgpr_waves(sgpr):
+    return 800 // (((sgpr + 15) // 16) * 16 + 16)
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("NW", [4, 8])
+def test_lap_residency_sgpr_cap(tsa, meta, M, NW):
+    """lap_sgpr_blocks_per_cu(M, NW, f16, sop) = SGPR waves per SIMD over the
+    waves a workgroup may put on one SIMD, from the table's worst variant."""
+    fn = getattr(tsa.lib(), "_ZN3tsa22lap_sgpr_blocks_per_cuEiibb")
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_bool, ctypes.c_bool]
+    for f16 in (False, True):
+        for sop in (False, True):
+            pre = f"_ZN3tsa10lap_kernelILi{M}ELi{NW}ELb{int(f16)}ELb{int(sop)}ELb0E"
+            sg = max(v["sgpr"] for k, v in meta.items() if k.startswith(pre))
+            want = sgpr_waves(sg) // ((NW + 1 + 3) // 4)
+            assert fn(M, NW, f16, sop) == want
+            assert want >= 1
+    # the edge the guide names: 97-112 SGPRs leave 6 waves per SIMD, 7 below it
+    assert sgpr_waves(106) == 6 and sgpr_waves(80) == 8
