@@ -593,7 +593,10 @@ def rtl_envelope(la: int, lb: int, lc: int, a_total_len: int = 512, pe_len: int 
 
     2cyc (TRIALIGN_2cyc, the ASIC variant): multiples of PE_LEN, LA <= 512
     (z SRAM depth, src/TriAlign_2cyc.v:135), and a y-face store whose pencil
-    slots never share an SRAM bank they must not share (`_rtl2_ring_ok`)."""
+    slots never share an SRAM bank they must not share (`_rtl2_ring_ok`).
+    The 2cyc rule is MODEL-DERIVED: it reproduces where the one cycle-level
+    transliteration (oracle/rtl_model_2cyc.c) agrees, and no Verilog
+    simulation has confirmed the shapes it rejects."""
     base = (la % pe_len == 0 and lb % pe_len == 0 and lc % pe_len == 0 and 0 < la <= a_total_len
             and lb > 0 and lc > 0)
     if variant == "1cyc":

@@ -6,8 +6,10 @@ inputs inside the RTL envelope, from the cycle-level RTL model
 (oracle/rtl_model.c); the script asserts the two agree before writing. Every
 default-parameter case with lengths that are multiples of 8 (LA <= 512) also
 records the 2-cycle RTL model's result (oracle/rtl_model_2cyc.c) and whether
-it agrees -- the 2-cycle variant's y-face SRAM banking breaks some shapes,
-non-power-of-two cubes among them.
+it agrees -- by that model the 2-cycle variant's y-face SRAM banking breaks
+some shapes, non-power-of-two cubes among them. Those
+`rtl2_model` records are MODEL-DERIVED: one transliteration of the RTL, not
+confirmed by a Verilog simulation (none exists in the image).
 Inputs: the reference's own dat triple (dat/{A,B,C}_seq.dat, copied as
 numbers), the testbench's all-A input (src/TriAlign_tb.sv:423-1960), prefixes,
 homopolymers, seeded random triples (uniform + related), RTL and SOP scoring,
@@ -26,6 +28,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import oracle  # noqa: E402
 
 REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+RTL2_SOURCE = "model-derived: oracle/rtl_model_2cyc.c transliteration, unverified by simulation"
 
 
 def read_dat(path):
@@ -51,7 +54,8 @@ def case(name, a, b, c, **pk):
         rec["rtl_model"] = {"score": r, "cycles": cyc}
     if default and all(n % 8 == 0 for n in (len(a), len(b), len(c))) and len(a) <= 512:
         r2, isx2, cyc2 = oracle.rtl2_run(a, b, c)
-        rec["rtl2_model"] = {"score": r2, "x": isx2, "cycles": cyc2, "agrees": (not isx2) and r2 == s}
+        rec["rtl2_model"] = {"score": r2, "x": isx2, "cycles": cyc2, "agrees": (not isx2) and r2 == s,
+                             "source": RTL2_SOURCE}
     return rec
 
 
@@ -98,7 +102,7 @@ def main():
         a, b, c = (r3.integers(0, 4, n).astype(np.uint8) for n in (la, lb, lc))
         cases.append(case(f"cube2_{la}x{lb}x{lc}", a, b, c))
     out = {"generator": "tests/golden/make_golden.py", "oracle": "oracle/tsa_oracle.c (+ rtl_model.c, rtl_model_2cyc.c)",
-           "cases": cases}
+           "rtl2_model_source": RTL2_SOURCE, "cases": cases}
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.json")
     with open(path, "w") as f:
         json.dump(out, f, separators=(",", ":"))
