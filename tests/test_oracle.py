@@ -64,7 +64,9 @@ def test_rtl2_model_testbench_and_dat(orc, golden):
     # A_idx + 16 steps (src/TriAlign_2cyc.v:354-355,433-482)
     assert cyc == 64 * (65 + 2 * (64 + 16)) + 1
     by = {c["name"]: c for c in golden}
-    assert by["dat"]["rtl2_model"] == {"score": 1, "x": False, "cycles": cyc, "agrees": True}
+    assert by["dat"]["rtl2_model"] == {"score": 1, "x": False, "cycles": cyc, "agrees": True,
+                                       "source": by["dat"]["rtl2_model"]["source"]}
+    assert by["dat"]["rtl2_model"]["source"].startswith("model-derived")
 
 
 def test_golden_rtl2_records(orc, golden, tsa):
