@@ -72,6 +72,7 @@ struct PencilArgs {
   // lam*(x+y+z); lam = GE = -MISMATCH, f16 bits in both halves
   int32_t lam;                  // lam as an integer (0: not V-space)
   uint32_t v_lam, v_cP, v_dO;   // lam, GO + MISMATCH + lam, GO - GE
+  float d0f, d1f;               // RTL s3 deltas (V-space K = (d0 + [b=c] d1) / code(b))
 };
 
 
@@ -161,6 +162,19 @@ __device__ __forceinline__ void lds_write16(uint8_t *p, uint4 v) {
   __attribute__((address_space(3))) u32x4_lds *q =
       (__attribute__((address_space(3))) u32x4_lds *)(__attribute__((address_space(3))) void *)p;
   *q = (u32x4_lds){v.x, v.y, v.z, v.w};
+}
+// The same through an LDS base pointer plus a byte offset: a compile-time
+// offset folds into the ds instruction's offset field (no VALU address add)
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+__device__ __forceinline__ lds_u8 *to_lds(uint8_t *p) {
+  return (lds_u8 *)(__attribute__((address_space(3))) void *)p;
+}
+__device__ __forceinline__ uint4 lds_read16_at(const lds_u8 *base, int off) {
+  const u32x4_lds v = *(const __attribute__((address_space(3))) u32x4_lds *)(base + off);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void lds_write16_at(lds_u8 *base, int off, uint4 v) {
+  *(__attribute__((address_space(3))) u32x4_lds *)(base + off) = (u32x4_lds){v.x, v.y, v.z, v.w};
 }
 __device__ __forceinline__ uint32_t ror1(uint32_t v) {  // lane l <- lane l-1, lane 0 <- lane 63
   // mov_dpp (old = undef): wave_ror:1 reads a valid lane for every lane
@@ -353,26 +367,28 @@ __device__ __forceinline__ void cell_messages_f16(
 //    axes, src/PE_1cyc.v:172-194, so max(Ixy', Ixz') covers every other source):
 //      Ix' = max(Ix - lam, max(Ixy', Ixz') - (GO + MISMATCH + lam));
 //  * M adds no constant: 3 MISMATCH + 3 lam = 0 (the SOP form folds 3 lam into K).
-// 25 instructions per pair (RTL) against cell_messages_f16's 33. Zero faces
+// 24 instructions per pair (RTL) against cell_messages_f16's 33. Zero faces
 // become lam*q at coordinate sum q: the kernel injects those (pencil_kernel.hip).
 template <int M, bool SOP>
 __device__ __forceinline__ void cell_messages_vs(
     const uint32_t (&a)[M], const uint32_t (&b)[M], const uint32_t (&c)[M],
-    const uint32_t (&SBC)[M], const uint32_t (&K)[M], const uint32_t (&DMC)[M], uint32_t Q,
+    const uint32_t (&SBC)[M], const uint32_t (&K)[M], const uint32_t (&DMC)[M], const uint32_t (&DMB)[M],
     const PencilArgs &pa,
     const uint32_t (&inIx)[M], const uint32_t (&inIy)[M], const uint32_t (&inIz)[M],
     const uint32_t (&inIxy)[M], const uint32_t (&inIyz)[M], const uint32_t (&inIxz)[M],
     const uint32_t (&inM)[M], uint32_t (&nIx)[M], uint32_t (&oIy)[M], uint32_t (&oIz)[M],
     uint32_t (&oIxy)[M], uint32_t (&oIyz)[M], uint32_t (&oIxz)[M], uint32_t (&oBest)[M]) {
-  const h2 DM = H(pa.h_dm), LAM = H(pa.v_lam), CP = H(pa.v_cP), DO = H(pa.v_dO);
+  const h2 LAM = H(pa.v_lam), CP = H(pa.v_cP), DO = H(pa.v_dO);
 #pragma unroll
   for (int i = 0; i < M; ++i) {
-    const h2 eab = H(umin2(a[i] & b[i], Q)), eac = H(a[i] & c[i]), DMCi = H(DMC[i]);
-    const h2 sXY = hfma(eab, DM, H(inIxy[i]));  // src/PE_1cyc.v:159-161 (+mismatch folded)
+    // a & b is b's code on a match, 0 otherwise; DMB = dm / code(b) and (RTL) K
+    // = (d0 + [b=c] d1) / code(b) per position and row: the products are exact
+    const h2 eab = H(a[i] & b[i]), eac = H(a[i] & c[i]), DMCi = H(DMC[i]), DMBi = H(DMB[i]);
+    const h2 sXY = hfma(eab, DMBi, H(inIxy[i]));  // src/PE_1cyc.v:159-161 (+mismatch folded)
     const h2 sXZ = hfma(eac, DMCi, H(inIxz[i]));
     const h2 sYZ = H(inIyz[i]) + H(SBC[i]);
     h2 sM;                                       // src/PE_1cyc.v:162
-    if constexpr (SOP) sM = hfma(eab, DM, hfma(eac, DMCi, H(inM[i]))) + H(K[i]);
+    if constexpr (SOP) sM = hfma(eab, DMBi, hfma(eac, DMCi, H(inM[i]))) + H(K[i]);
     else sM = hfma(eab, H(K[i]), H(inM[i]));     // ne + 3 lam = 0
     const h2 sX = H(inIx[i]), sY = H(inIy[i]), sZ = H(inIz[i]);
     const h2 Gx = vmax3(sY, sZ, sYZ), Gy = vmax3(sX, sZ, sXZ), Gz = vmax3(sX, sY, sXY);
@@ -415,6 +431,16 @@ __device__ __forceinline__ void load_a(uint32_t va, uint32_t (&a)[M]) {
   for (int i = 0; i < M; ++i)
     a[i] = *(const __attribute__((address_space(3))) uint32_t *)(uintptr_t)(
         va + 4u * (uint32_t)(M - 1 - i));
+}
+// The same at a constant entry offset `off` from va, as an inbounds index of
+// an LDS pointer, so the offset folds into the ds_read's offset field (a u32
+// add could wrap, and the compiler then adds it in a VALU op)
+template <int M>
+__device__ __forceinline__ void load_a_off(uint32_t va, int off, uint32_t (&a)[M]) {
+  const __attribute__((address_space(3))) uint32_t *p =
+      (const __attribute__((address_space(3))) uint32_t *)(uintptr_t)va;
+#pragma unroll
+  for (int i = 0; i < M; ++i) a[i] = p[off + M - 1 - i];
 }
 // bfi mask selecting one half (hs) of one lane (ls): the lane bit comes from a
 // scalar shift, so this is one VALU op (v_cndmask with an SGPR-pair mask);

@@ -56,6 +56,10 @@ __host__ __device__ constexpr int helix_pd(int M) { return M >= 8 ? 2 : M >= 4 ?
 // skew and record slots per wave; M >= 4 keeps skew 1 (twice the slots would not fit LDS)
 __host__ __device__ constexpr int helix_skew(int M) { return M <= 2 ? TSA_SKEW : 1; }
 constexpr int RING_EXTRA = 8;
+// A-table entries past P + 128M repeating its start (the table is periodic in
+// P): the V-space loop reads a four-step group's A codes at constant offsets
+// from one address computed at the group's start, across a lap wrap too
+constexpr int A_PAD = 4;
 
 struct PencilGeom {
   int32_t M;        // pairs per lane
@@ -88,7 +92,7 @@ static PencilGeom pencil_geom(int32_t max_la, int32_t max_lc) {
 }
 static size_t helix_lds(int M, int NW, int32_t P, int32_t max_lb) {
   return (size_t)(NW - 1) * 2 * helix_skew(M) * M * 1024 + (size_t)helix_pd(M) * M * 1024 +
-         4 * ((size_t)P + 128 * M) + 4 * (((size_t)max_lb + 3) & ~(size_t)3) + (size_t)M * 512;
+         4 * ((size_t)P + 128 * M + A_PAD) + 4 * (((size_t)max_lb + 3) & ~(size_t)3) + (size_t)M * 512;
 }
 
 // The factored messages widen each target's highest-penalty group to all seven
@@ -245,6 +249,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
   const uint32_t a_lane = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)sA2 +
                           4u * (uint32_t)(ZT - M * lane - (M - 1));
 
+  // this lane's record slots: read from the wave above, written for the one
+  // below (LDS pointers, so the slot offsets fold into the ds instructions)
+  const lds_u8 *rd_base = to_lds(xr + (w > 0 ? (w - 1) * HNSL * SLOT_BYTES : 0) + lane * REC_BYTES);
+  lds_u8 *wr_base = to_lds(xr + w * HNSL * SLOT_BYTES + lane * REC_BYTES);
   const int32_t nunit = TWO ? (n + 1) / 2 : n;  // workgroup units: triples, or pairs
   for (int unit = blockIdx.x; unit < nunit; unit += gridDim.x) {
     const int tri = TWO ? 2 * unit : unit;
@@ -262,7 +270,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 
     // ---- stage A codes (padded to P, halves k/k+64M or, TWO, the two triples) and
     // B; face records in the ring
-    for (int j = threadIdx.x; j < P + ZT; j += 64 * NW) {
+    for (int j = threadIdx.x; j < P + ZT + A_PAD; j += 64 * NW) {  // periodic in j: the pad repeats P
       const int x0 = ((j - ZT) % P + P) % P, x1 = TWO ? x0 : ((j - ZT - 64 * M) % P + P) % P;
       const uint32_t c0 = x0 < la ? SYM0 << tsa_sym(seqs, o0 + x0, pa.packed) : 0u;
       const uint32_t c1 = x1 < la1 ? SYM0 << tsa_sym(seqs, (TWO ? q0 : o0) + x1, pa.packed) : 0u;
@@ -296,7 +304,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     __syncthreads();
 
     // ---- per-position registers (arrays [2] alternate roles between even/odd steps)
-    uint32_t b[M], c[M], SBC[M], K[M], DMC[M];
+    uint32_t b[M], c[M], SBC[M], K[M], DMC[M], DMB[M];
     uint32_t oIx[M], shIz[M], svIxy[M], svIyz[M], shIxz[2][M], svM[2][M];
 #pragma unroll
     for (int i = 0; i < M; ++i) {
@@ -305,7 +313,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       const uint32_t c1 = k1 < lc1 ? SYM0 << tsa_sym(seqs, (TWO ? q2 : o2) + k1, pa.packed) : 0u;
       c[i] = c0 | (c1 << 16);
       DMC[i] = dm_over_code(pa.dmf, c[i]);
-      b[i] = SBC[i] = K[i] = 0;  // set when a position reaches x = 1 of its lap
+      b[i] = SBC[i] = K[i] = DMB[i] = 0;  // set when a position reaches x = 1 of its lap
       oIx[i] = pa.f_single;
       shIz[i] = pa.f_single;
       shIxz[0][i] = shIxz[1][i] = pa.f_pair;
@@ -334,14 +342,25 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     uint32_t binj = b_of_lap(lap0);
     // the per-row terms of the row whose B code is binj, for every position:
     // a position copies them when it reaches x = 1 (recomputed once per lap)
-    uint32_t SBCn[M], Kn[M];
+    uint32_t SBCn[M], Kn[M], DMBn = 0;
     auto row_terms = [&]() {
       if constexpr (F16 && TSA_ROW_NEXT) {
+        // V-space: the [a=b] terms multiply the symbol code itself (a & b, no
+        // min): DMB = dm / code(b) and, RTL, K = (d0 + [b=c] d1) / code(b)
+        uint32_t kb0 = k0v, kbd = kdv;
+        if constexpr (VS) {
+          DMBn = dm_over_code(pa.dmf, binj);
+          if constexpr (!SOP) {
+            kb0 = dm_over_code(pa.d0f, binj);
+            const uint32_t kb1 = dm_over_code(pa.d0f + pa.d1f, binj);
+            kbd = (((kb1 & 0xFFFFu) - (kb0 & 0xFFFFu)) & 0xFFFFu) | ((((kb1 >> 16) - (kb0 >> 16)) & 0xFFFFu) << 16);
+          }
+        }
 #pragma unroll
         for (int i = 0; i < M; ++i) {
           const uint32_t e01 = pk_eq1(binj, c[i], one1);
           SBCn[i] = pk_mad(e01, sbcv, 0u);
-          Kn[i] = pk_mad(e01, kdv, k0v);
+          Kn[i] = pk_mad(e01, kbd, kb0);
         }
       }
     };
@@ -391,6 +410,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     uint32_t a_nx[M];                            // A codes of the coming step
     if constexpr (TSA_A_PREFETCH) load_a<M>(a_lane + 4u * (uint32_t)xpos0, a_nx);
     int32_t st_row = 0;                          // ring row written at step t (last wave)
+    uint32_t abase = a_lane;                     // VS: A address of the group's first step
 
     // One step; PH = t & 1 picks the register roles and the LDS record slots,
     // ROLE the wave's place in the lap (0: wave 0, reads the ring; 2: the last
@@ -422,10 +442,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll
         for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
       } else {
-        const uint8_t *src = xr + ((w - 1) * HNSL + (HSK == 2 ? (q + 2) & 3 : PH ^ 1)) * SLOT_BYTES +
-                             lane * REC_BYTES;
+        const int off = (HSK == 2 ? (q + 2) & 3 : PH ^ 1) * SLOT_BYTES;
 #pragma unroll
-        for (int i = 0; i < M; ++i) rec[i] = lds_read16(src + i * PAIR_BYTES);
+        for (int i = 0; i < M; ++i) rec[i] = lds_read16_at(rd_base, off + i * PAIR_BYTES);
       }
       uint32_t inIx[M], inIy[M], inIz[M], inIxy[M], inIyz[M], inIxz[M], inM[M];
 #pragma unroll
@@ -471,6 +490,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #if TSA_ROW_NEXT
               SBC[i] = vbfi(m1, SBCn[i], SBC[i]);
               K[i] = vbfi(m1, Kn[i], K[i]);
+              if constexpr (VS) DMB[i] = vbfi(m1, DMBn, DMB[i]);
 #else
               const uint32_t e01 = pk_eq1(b[i], c[i], one1);
               SBC[i] = pk_mad(e01, sbcv, 0u);
@@ -484,7 +504,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       // this the allocator copies b into a fresh pair every step)
 #if TSA_PIN_ROW
 #pragma unroll
-      for (int i = 0; i < M; ++i) asm volatile("" : "+v"(b[i]), "+v"(SBC[i]), "+v"(K[i]));
+      for (int i = 0; i < M; ++i) asm volatile("" : "+v"(b[i]), "+v"(SBC[i]), "+v"(K[i]), "+v"(DMB[i]));
 #endif
       uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
       // Priority 0 for the cell arithmetic, 1 for the send/shift/barrier tail:
@@ -493,7 +513,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       if constexpr (TSA_SETPRIO) __builtin_amdgcn_s_setprio(0);
       if constexpr (TSA_SCHED_FENCE) __builtin_amdgcn_sched_barrier(0);  // keep the arithmetic between the two
       if constexpr (VS)
-        cell_messages_vs<M, SOP>(a, b, c, SBC, K, DMC, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx,
+        cell_messages_vs<M, SOP>(a, b, c, SBC, K, DMC, DMB, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx,
                                  oIy, oIz, oIxy, oIyz, oIxz, oBest);
       else if constexpr (F16)
         cell_messages_f16<M, SOP>(a, b, c, SBC, K, DMC, ones, pv, inIx, inIy, inIz, inIxy, inIyz, inIxz, inM, nIx,
@@ -523,10 +543,10 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 
       // ---- send this step's record to the wave below (or the ring)
       if constexpr (ROLE != 2) {
-        uint8_t *dst = xr + (w * HNSL + (HSK == 2 ? q : PH)) * SLOT_BYTES + lane * REC_BYTES;
+        const int off = (HSK == 2 ? q : PH) * SLOT_BYTES;
 #pragma unroll
         for (int i = 0; i < M; ++i)
-          lds_write16(dst + i * PAIR_BYTES, make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
+          lds_write16_at(wr_base, off + i * PAIR_BYTES, make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
       } else {
         // Positions that have not started (u = t - w - k < 0) must publish the
         // y = 0 face: wave 0 reads this row as "row y0-1" during its lap 0.
@@ -603,7 +623,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         zshift<M>(svM[PH], rw, sel, 0u);
         advance();
       }
-      if constexpr (TSA_A_PREFETCH) load_a<M>(a_lane + 4u * (uint32_t)xpos0, a_nx);
+      if constexpr (VS) load_a_off<M>(abase, (PQ & 3) + 1, a_nx);  // x' of step t + 1
+      else if constexpr (TSA_A_PREFETCH) load_a<M>(a_lane + 4u * (uint32_t)xpos0, a_nx);
 
       // ---- wave 0: fetch the record of step t + PD into the slot just consumed
       if constexpr (ROLE == 0) {
@@ -638,6 +659,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       if constexpr (VS) {  // whole groups of four steps (H's phase is t & 3), the final cell tested
 #pragma unroll 1
         for (; t < T; t += 4) {
+          abase = a_lane + 4u * (uint32_t)xpos0;
           TSA_INLINE_IF_WIDE(step(Q0, role, t, mid));
           TSA_INLINE_IF_WIDE(step(Q1, role, t + 1, mid));
           TSA_INLINE_IF_WIDE(step(Q2, role, t + 2, mid));
@@ -751,6 +773,8 @@ PencilArgs make_args(const KParams &kp, bool f16, bool vs) {
     a.v_lam = pkh(GE);
     a.v_cP = pkh(GO + mm + GE);
     a.v_dO = pkh(GO - GE);
+    a.d0f = (float)d0;
+    a.d1f = (float)d1;
     if (a.sop) {
       const uint32_t k0v = pkh(3.0 * mm + 3.0 * GE), k1v = pkh(3.0 * mm + dm + 3.0 * GE);
       a.h_k0 = k0v;
@@ -806,7 +830,7 @@ static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                     const PencilArgs &pa, hipStream_t stream) {
   constexpr bool VSOK = F16 && M <= 2;  // V-space instantiations
   const bool vs = VSOK && pa.lam != 0;
-  const int32_t lds_a = 4 * (g.P + 128 * M), lds_b = 4 * ((max_lb + 3) & ~3);
+  const int32_t lds_a = 4 * (g.P + 128 * M + A_PAD), lds_b = 4 * ((max_lb + 3) & ~3);
   const size_t lds = helix_lds(M, NW, g.P, max_lb);
   // TWO (two triples per workgroup) exactly when pencil_geom sized P for it
   const bool two = M == 1 && g.two;

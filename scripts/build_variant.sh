@@ -21,6 +21,11 @@ for f in $SRC/csrc/*.hip; do
   objs+=("$o")
 done
 wait
-/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -shared -o "$OUT/lib/libtrialign.so" "${objs[@]}" -lpthread
+for o in "${objs[@]}"; do [ -f "$o" ] || { echo "build_variant: $o failed" >&2; exit 1; }; done
+# the kernel resource table (tools/kernel_meta.py; a tree without it links it unused)
+python3 $PKG/tools/kernel_meta.py --cpp "$OUT/build/kernel_meta.cpp" "${objs[@]}" > /dev/null
+g++ -O2 -std=c++17 -fPIC -I$PKG/csrc -c "$OUT/build/kernel_meta.cpp" -o "$OUT/build/kernel_meta.o"
+/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -fPIC -shared -o "$OUT/lib/libtrialign.so" "${objs[@]}" \
+  "$OUT/build/kernel_meta.o" -lpthread
 rm -rf "$OUT/build"
 echo "built $OUT"
