@@ -99,9 +99,10 @@ static size_t lap_lds_bytes(int M, int NW, int32_t max_la) {
 
 // Trace slots per block (TSA_LAP_TRACE): 8, plus with TSA_DIAG (the
 // diagnostic build, scripts/build_variant.sh) 4 shader-clock accumulators per
-// compute wave.
+// compute wave and the largest producer-consumer lag (steps) seen by the y and
+// z stores -- the ring slots that workgroup needed.
 #if defined(TSA_DIAG)
-constexpr int LAP_TRACE_SLOTS = 8 + 4 * 8;
+constexpr int LAP_TRACE_SLOTS = 8 + 4 * 8 + 2;
 #else
 constexpr int LAP_TRACE_SLOTS = 8;
 #endif
@@ -665,6 +666,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
     uint32_t n_bp = 0;
 #if defined(TSA_DIAG)  // shader cycles: reads + pre-cell, check, post + stores, step gap
     uint64_t prof[4] = {0, 0, 0, 0}, prof_last = 0;
+    int32_t lag_y = 0, lag_z = 0;  // t - the consumer's progress, at the ring stores
 #endif
     constexpr int LM = M == 1 ? 0 : M == 2 ? 1 : M == 4 ? 2 : 3;  // log2 M
     int32_t klo = -2 * w, ihi = 0;  // x = 1 position of the low half at the current step
@@ -842,6 +844,9 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
           lds_write16(dst + i * PAIR, make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
       } else {
         if (yout) {
+#if defined(TSA_DIAG)
+          lag_y = max(lag_y, t - prog_decode(lds_word(bpw)));
+#endif
           wait_consumer(cons_y, seen_y, bpw, t - YR - YOFF + 1);
           const uint32_t tg = lap_tag(epoch, t);
 #pragma unroll
@@ -863,6 +868,9 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       }
       // ---- z record of this wave's last position (lane 63, register M-1)
       if (zout) {
+#if defined(TSA_DIAG)
+        lag_z = max(lag_z, t - prog_decode(lds_word(bpw + 1)));
+#endif
         wait_consumer(cons_z, seen_z, bpw + 1, t - ZR - ZT - ZA + 1);
         if (lane == 63) {
           const uint32_t tg = lap_tag(epoch, t);
@@ -950,6 +958,10 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
 #if defined(TSA_DIAG)
     if (trace != nullptr && lane == 0 && w < 8)
       for (int k = 0; k < 4; ++k) trace[(int64_t)b * LAP_TRACE_SLOTS + 8 + 4 * w + k] = prof[k];
+    if (trace != nullptr && lane == 0) {
+      atomicMax(trace + (int64_t)b * LAP_TRACE_SLOTS + 40, (unsigned long long)max(lag_y, 0));
+      atomicMax(trace + (int64_t)b * LAP_TRACE_SLOTS + 41, (unsigned long long)max(lag_z, 0));
+    }
 #endif
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1169,8 +1181,9 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
     (void)hipFree(trace);
     if (FILE *fp = fopen(tpath, "w")) {
       fprintf(fp, "block,tri,lap,tile,start,loop_begin,loop_end,xcc,stalls,w0_waits,loop_clk,bp_waits");
-      for (int k = 8; k < LAP_TRACE_SLOTS; ++k)  // TSA_DIAG: wave (k-8)/4, phase (k-8)%4
+      for (int k = 8; k < 40 && k < LAP_TRACE_SLOTS; ++k)  // TSA_DIAG: wave (k-8)/4, phase (k-8)%4
         fprintf(fp, ",prof%d_%d", (k - 8) / 4, (k - 8) % 4);
+      if (LAP_TRACE_SLOTS > 40) fprintf(fp, ",lag_y,lag_z");
       fprintf(fp, "\n");
       for (int64_t b = 0; b < g.blocks; ++b) {
         const unsigned long long *hb = h.data() + b * LAP_TRACE_SLOTS;

@@ -14,6 +14,6 @@ for L in 64 128 256; do
   done
 done
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-TSA_PENCIL_MODE=literal timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o lit -- python tools/bench_variants.py --kernel plane --n 512 --L 256 --rounds 5 --variants TSA_PENCIL_MODE=literal > $OUT/prof.log 2>&1 || exit 1
+TSA_PENCIL_MODE=literal timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o lit --output-format csv -- python tools/bench_variants.py --kernel plane --n 512 --L 256 --rounds 5 --variants TSA_PENCIL_MODE=literal > $OUT/prof.log 2>&1 || exit 1
 find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/literal_kernel_stats.csv \;
 cat $OUT/batch.jsonl $OUT/single.jsonl

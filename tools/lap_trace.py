@@ -145,6 +145,18 @@ def main():
                         parts.append(round(statistics.median(vals), 1))
                     prof[f"w{wv}"] = parts
                 rec["prof_clk_per_step"] = {"phases": "reads+pre, check, post+stores, gap", **prof}
+            if "lag_y" in rows[0]:  # TSA_DIAG: the ring slots each workgroup needed
+                for key in ("lag_y", "lag_z"):
+                    vals = sorted(int(r[key]) for r in rows)
+                    by_tile, by_lap = {}, {}
+                    for r in rows:
+                        v, tl, lp = int(r[key]), int(r["tile"]), int(r["lap"])
+                        by_tile[tl] = max(by_tile.get(tl, 0), v)
+                        by_lap[lp] = max(by_lap.get(lp, 0), v)
+                    q = lambda f: vals[min(len(vals) - 1, int(f * len(vals)))]
+                    rec[key] = {"max": vals[-1], "p50": q(0.5), "p90": q(0.9), "p99": q(0.99),
+                                "by_tile": [by_tile[k] for k in sorted(by_tile)],
+                                "by_lap_q": [by_lap[k] for k in sorted(by_lap)][:: max(1, len(by_lap) // 16)]}
         print(json.dumps(rec), flush=True)
 
 
