@@ -71,7 +71,18 @@ bool literal_helix_chosen(int32_t n, int32_t max_la, int32_t max_lb, int32_t max
     if (!strcmp(e, "plane")) return false;
     if (!strcmp(e, "literal")) return true;
   }
-  return n >= 16;  // a single cube runs faster as a plane sweep over the whole chip
+  // Cost model fitted on MI355X (profiles/r3d_literal_vs_plane.jsonl): the
+  // literal helix runs T steps of 0.56 us (M = 1) / 0.95 us (M = 2) per
+  // workgroup, ~1.8x slower per step with two workgroups on every CU; PLANE
+  // runs LA+LB+LC plane launches of 4.4 us + 0.41 us per triple per 256^2
+  // (y,z) cells. A few large cubes sweep faster as planes over the chip.
+  const LitGeom g = lit_geom(max_la, max_lb, max_lc);
+  const double T = (double)((max_lb + LIT_NW - 1) / LIT_NW) * g.P + LIT_S * (LIT_NW - 1) + max_lc;
+  const double waves = n > 256 ? 1.8 * (double)((n + 511) / 512) : 1.0;
+  const double lit_us = T * (g.M == 1 ? 0.56 : 0.95) * waves;
+  const double plane_us = (double)(max_la + max_lb + max_lc) *
+                          (4.4 + 0.41 * (double)n * (double)max_lb * (double)max_lc / 65536.0);
+  return lit_us <= plane_us;
 }
 size_t literal_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
   return (size_t)std::min<int32_t>(n, 65535) * (size_t)lit_geom(max_la, max_lb, max_lc).ring_bytes_per_triple;

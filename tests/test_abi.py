@@ -67,8 +67,12 @@ def test_validate(tsa):
     assert tsa.validate([0] * 20, [0] * 20, [0] * 20, big) == tsa.TSA_ERANGE
 
 
-def test_workspace_size(tsa):
+def test_workspace_size(tsa, monkeypatch):
     p = tsa.TsaParams.default()
+    # the literal helix: one ring of (P + 8) records x M x 64 lanes x 16 B per triple
+    lit = tsa.workspace_size(4, 64, 64, 64, p, "plane")
+    assert lit == 4 * (128 + 8) * 64 * 16
+    monkeypatch.setenv("TSA_PENCIL_MODE", "plane")  # the plane sweep itself
     n1 = tsa.workspace_size(1, 64, 64, 64, p, "plane")
     n4 = tsa.workspace_size(4, 64, 64, 64, p, "plane")
     assert n4 == 4 * n1 and n1 >= 4 * 7 * 65 * 65 * 2
@@ -108,10 +112,15 @@ def test_describe_plan(tsa):
     assert tsa.describe_plan(1, 1024, 1024, 1024, p16).startswith("pencil lap i16 rtl")
     sop = tsa.TsaParams.default(s3_mode=tsa.S3_SOP)
     assert " sop " in tsa.describe_plan(512, 256, 256, 256, sop)
-    assert tsa.describe_plan(4, 64, 64, 64, p, kernel="plane") == "plane"
-    # gap_extend > gap_open: the widened message groups are not exact -> plane
+    # the literal kernels: the literal helix where its cost model beats the
+    # plane sweep (small cubes, batches), PLANE for a few large cubes
+    assert tsa.describe_plan(4, 64, 64, 64, p, kernel="plane") == "plane literal-helix"
+    assert tsa.describe_plan(512, 256, 256, 256, p, kernel="plane") == "plane literal-helix"
+    assert tsa.describe_plan(1, 256, 256, 256, p, kernel="plane") == "plane"
+    assert tsa.describe_plan(4, 512, 512, 512, p, kernel="plane") == "plane"  # LC > 256
+    # gap_extend > gap_open: the widened message groups are not exact -> literal
     ge = tsa.TsaParams.default(gap_open=1, gap_extend=2)
-    assert tsa.describe_plan(4, 64, 64, 64, ge) == "plane"
+    assert tsa.describe_plan(4, 64, 64, 64, ge) == "plane literal-helix"
     with pytest.raises(tsa.TsaError) as e:
         tsa.describe_plan(4, 64, 64, 64, ge, kernel="pencil")
     assert e.value.rc == tsa.TSA_ERANGE
@@ -119,7 +128,7 @@ def test_describe_plan(tsa):
     # the synchronous path tries the checked lap kernel first (PLANE rescoring
     # whatever it cannot certify), and so does an explicit kernel="checked"
     p6 = tsa.TsaParams.default(score_bits=6)
-    assert tsa.describe_plan(4, 90, 90, 90, p6, sync=False) == "plane"
+    assert tsa.describe_plan(4, 90, 90, 90, p6, sync=False) == "plane literal-helix"
     assert tsa.describe_plan(4, 90, 90, 90, p6, sync=True).endswith(" checked")
     assert tsa.describe_plan(1, 1024, 1024, 1024, p, sync=True).startswith("pencil lap i16 rtl")
     assert tsa.describe_plan(1, 1024, 1024, 1024, p, sync=False) == "plane"

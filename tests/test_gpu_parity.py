@@ -10,6 +10,16 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 KERNELS = ["plane", "pencil", "auto"]
+# "plane" runs the literal helix where its cost model picks it (small cubes,
+# batches); "plane-sweep" forces the PLANE sweep itself (TSA_PENCIL_MODE=plane)
+LITERAL_KERNELS = ["plane", "plane-sweep", "pencil", "auto"]
+
+
+def _select(kernel, monkeypatch):
+    if kernel == "plane-sweep":
+        monkeypatch.setenv("TSA_PENCIL_MODE", "plane")
+        return "plane"
+    return kernel
 
 
 def _kernel_applies(tsa, kernel, la, lb, lc, p):
@@ -25,8 +35,9 @@ def _kernel_applies(tsa, kernel, la, lb, lc, p):
         return False
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
-def test_golden_fixtures(gpu, golden, kernel):
+@pytest.mark.parametrize("kernel", LITERAL_KERNELS)
+def test_golden_fixtures(gpu, golden, kernel, monkeypatch):
+    kernel = _select(kernel, monkeypatch)
     used = 0
     for c in golden:
         p = gpu.TsaParams.default(**c["params"])
@@ -61,9 +72,10 @@ def test_testbench_input_and_dat_cli(gpu, golden):
     assert r.stdout.strip().split()[-1] == "1"
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("kernel", LITERAL_KERNELS)
 @pytest.mark.parametrize("s3_mode,bits", [(0, 12), (1, 12), (0, 0), (0, 16), (1, 9)])
-def test_random_small_vs_oracle(gpu, orc, kernel, s3_mode, bits):
+def test_random_small_vs_oracle(gpu, orc, kernel, s3_mode, bits, monkeypatch):
+    kernel = _select(kernel, monkeypatch)
     rng = np.random.default_rng(1000 * s3_mode + bits)
     p = gpu.TsaParams.default(s3_mode=s3_mode, score_bits=bits)
     op = orc.default_params(s3_mode=s3_mode, score_bits=bits)
