@@ -8,26 +8,36 @@ namespace tsa {
 
 struct PencilArgs;
 
+// Dispatch rounds of a lap grid (kernel argument): blocks run per XCD in block
+// order, SX slots at a time; a producer whose consumer is in a later round
+// writes a full-length ring (YRB / ZRB slots) in the boundary regions yb / zb
+// (KBY rings per column for y, one per round boundary for z).
+struct LapRounds {
+  int32_t SX, KBY, YRB, ZRB;
+  uint8_t *yb, *zb;
+};
+
 struct LapGeom {
   int32_t M, NW;     // packed pairs per lane (tile = 64 M positions), waves (2 NW rows)
   int32_t G, GZ;     // laps, z-tiles
   int32_t NC, CH;    // columns (triple, z-tile) and columns per XCD (blocks = G * CH * 8)
-  int32_t YR, ZR;    // y / z ring slots per workgroup (powers of 2)
-  int32_t per_cu;    // workgroups a CU holds (occupancy API on the kernel)
+  int32_t YR, ZR;    // slim y / z ring slots per workgroup (powers of 2)
+  int32_t SX, KBY, KBZ, YRB, ZRB;  // rounds: slots per XCD, boundary rings (LapRounds)
+  int32_t per_cu;    // workgroups a CU holds (per-SIMD register model, occupancy API)
   int64_t blocks;    // grid (padding blocks for the XCD-aware tile mapping)
-  size_t lds, prog_bytes, yf_bytes, zf_bytes;
-  int64_t waves;     // dispatch waves: 1 = every workgroup resident at once
+  size_t lds, prog_bytes, yf_bytes, zf_bytes, yb_bytes, zb_bytes;
+  int64_t waves;     // dispatch rounds: 1 = every workgroup resident at once
   double est_us;     // estimated latency
   bool ok;           // feasible and more than one workgroup per triple
 };
 
-// A grid beyond the resident slots runs in dispatch waves; streaming is
-// limited to a few of them.
+// A grid beyond the resident slots runs in dispatch rounds (boundary rings
+// keep a producer from waiting on a later round); limited to a few.
 constexpr int64_t LAP_MAX_WAVES = 3;
 
 // Geometry of the lap schedule (M pairs per lane, NW waves) for a batch of n
-// triples; full_rings: rings as long as the cube (no back-pressure -- the form a
-// grid beyond the resident slots needs).
+// triples; full_rings: every ring as long as the cube (no back-pressure: the
+// split over devices, whose parts may queue behind each other).
 LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW,
                  bool full_rings, bool f16, bool sop);
 size_t lap_workspace_bytes(const LapGeom &g);

@@ -45,9 +45,11 @@
 //    hold 2-4x the natural lag);
 //  * block b -> XCD b % 8 (observed dispatch, speed only): every lap of a z-tile
 //    lands on one XCD, so the y chain's hand-offs stay in one L2's reach.
-// A workgroup only waits on workgroups of lower block index (lap-major order),
-// so a grid beyond the resident slots is safe with in-order dispatch when the
-// rings are full length (no back-pressure): LAP_STREAM uses that.
+// A consumer only waits on workgroups of lower block index (lap-major order),
+// and a producer waits (back-pressure) only on a consumer of its own dispatch
+// round -- across a round boundary its ring is full length -- so a grid beyond
+// the resident slots is safe with per-XCD in-order dispatch (measured, not
+// promised by HIP; every wait is bounded and reports).
 
 #include <unistd.h>
 
@@ -297,11 +299,16 @@ __device__ __forceinline__ void lap_post_i16(const PencilArgs &pa, const uint32_
 //   pw    [NW+1][64] i32        progress words (steps done): compute wave w, loader NW
 //   fin   [M][64] u32           best of the final step
 //   sA2   [..] u32              A code pairs: entry j = x j-OFF (lo), j-OFF-1 (hi)
-// Minimum waves per SIMD the register allocation must allow: pins occupancy
-// (and keeps SGPRs <= ~80, which the CU's admission of 256-thread blocks also
-// depends on, MI355X_MICROARCH.md "Residency"), so the occupancy API's answer
-// is what the hardware admits and a resident grid stays resident.
-__host__ __device__ constexpr int lap_waves_per_eu(int M) { return M == 1 ? 4 : M == 2 ? 5 : 2; }
+// Minimum waves per SIMD the register allocation must allow. A workgroup's
+// NW + 1 waves may sit ceil((NW + 1) / 4) to a SIMD (the dispatcher need not
+// balance them), so two NW = 8 workgroups per CU need 6 waves per SIMD, i.e.
+// <= 80 VGPRs: with 96 (5 waves) the CU admitted one, and the second half of
+// a 1024^3 lap grid started only as the first half finished (ring-lag census,
+// profiles/r3e_lap_lag.jsonl). M = 1 fits 6 as it is; M >= 4 runs one per CU.
+#ifndef TSA_LAP_WPE2
+#define TSA_LAP_WPE2 5
+#endif
+__host__ __device__ constexpr int lap_waves_per_eu(int M) { return M == 1 ? 4 : M == 2 ? TSA_LAP_WPE2 : 2; }
 // f(integral_constant<J>) for J = B .. E-1, unrolled at compile time
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F &&f) {
@@ -330,7 +337,7 @@ template <int M, int NW, bool F16, bool SOP, bool CHK, bool SYS = false>
 __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel(
     const uint8_t *__restrict__ seqs, const int64_t *__restrict__ offs, int32_t G, int32_t GZ,
     int32_t NC, int32_t CH, int32_t YR, int32_t ZR, uint8_t *__restrict__ yf_base,
-    uint8_t *__restrict__ zf_base, int32_t *__restrict__ prog, uint32_t *__restrict__ err,
+    uint8_t *__restrict__ zf_base, LapRounds rd, int32_t *__restrict__ prog, uint32_t *__restrict__ err,
     int32_t *__restrict__ scores, int32_t *__restrict__ mon, PencilArgs pa, uint32_t epoch,
     uint32_t spin_limit, int32_t L0, int32_t L1, uint8_t *__restrict__ yf_out,
     int32_t *__restrict__ prog_in,
@@ -394,13 +401,38 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
   const int32_t T = final_wg ? (la - 1) + tau(r_f) + k_f + 1 : la + tau(rows - 1) + zt_q - 1;
   const int32_t T_above = la + tau(RW - 1) + zt_q - 1;  // records the lap above writes (same tile)
   const int32_t T_left = la + tau(rows - 1) + ZT - 1;   // z records the tile to the left writes
-  uint8_t *yf_mine = (L == L1 - 1 ? yf_out : yf_base) + lid * YR * SLOT;  // in my consumer's memory
+  // Rings. A grid beyond the resident slots runs in dispatch rounds (per XCD,
+  // in block order: rd.SX slots each). A producer whose consumer is in a later
+  // round gets a full-length ring from the boundary region (it never waits
+  // for a consumer that may not have started); all others a slim ring of
+  // YR / ZR slots, their consumers co-resident (lap_geom).
+  const int32_t ch = slot % CH, xc = b & 7;
+  auto round_of = [&](int32_t s) { return s / rd.SX; };
+  auto y_bidx = [&](int32_t Lp, int32_t sp) {  // boundary index of producer (Lp, my column), or -1
+    const int32_t sc = sp + CH;
+    if (round_of(sc) == round_of(sp)) return -1;
+    return (int32_t)(((int64_t)col * rd.KBY) + (CH >= rd.SX ? Lp - L0 : round_of(sp) - round_of(ch)));
+  };
+  auto z_bidx = [&](int32_t sp, int32_t xp) {  // boundary index of producer (slot sp, XCD xp), or -1
+    return (xp == 7 && round_of(sp + 1) != round_of(sp)) ? round_of(sp) : -1;
+  };
+  const int32_t yb_me = yout ? y_bidx(L, slot) : -1, yb_pr = yin ? y_bidx(L - 1, slot - CH) : -1;
+  const int32_t zb_me = zout ? z_bidx(slot, xc) : -1;
+  const int32_t zb_pr = zin ? (xc == 0 ? z_bidx(slot - 1, 7) : -1) : -1;
+  const int32_t YRm = yb_me >= 0 ? rd.YRB : YR, YRp = yb_pr >= 0 ? rd.YRB : YR;
+  const int32_t ZRm = zb_me >= 0 ? rd.ZRB : ZR, ZRp = zb_pr >= 0 ? rd.ZRB : ZR;
+  uint8_t *yf_mine = yb_me >= 0 ? rd.yb + (int64_t)yb_me * rd.YRB * SLOT
+                                : (L == L1 - 1 ? yf_out : yf_base) + lid * YR * SLOT;  // in my consumer's memory
   // my progress word: read by the z producer (same part, local) and the y
   // producer -- at lap L0 of a split cube the previous part, so a copy goes there
   int32_t *const prog_x = (SYS && L == L0 && L0 > 0) ? prog_in + lid * LAP_PROG_STRIDE : nullptr;
-  const uint8_t *yf_prev = yin ? yf_base + (lid - GZ) * YR * SLOT : yf_mine;
-  uint8_t *zf_mine = zf_base + lid * ZR * ZREC;
-  const uint8_t *zf_prev = zin ? zf_base + (lid - 1) * ZR * ZREC : zf_mine;
+  const uint8_t *yf_prev = !yin ? yf_mine
+                           : yb_pr >= 0 ? rd.yb + (int64_t)yb_pr * rd.YRB * SLOT
+                                        : yf_base + (lid - GZ) * YR * SLOT;
+  uint8_t *zf_mine = zb_me >= 0 ? rd.zb + (int64_t)zb_me * rd.ZRB * ZREC : zf_base + lid * ZR * ZREC;
+  const uint8_t *zf_prev = !zin ? zf_mine
+                           : zb_pr >= 0 ? rd.zb + (int64_t)zb_pr * rd.ZRB * ZREC
+                                        : zf_base + (lid - 1) * ZR * ZREC;
   const uint32_t ep19 = epoch & 0x7FFFFu;
   bool timed_out = false;
   auto fail = [&]() {  // every wait of this workgroup gives up from now on
@@ -475,13 +507,13 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       const int32_t r = s + YOFF;
 #pragma unroll
       for (int i = 0; i < M; ++i) {
-        const uint8_t *g = yf_prev + ((int64_t)(r & (YR - 1)) * M + i) * PAIR + lane * REC_BYTES;
+        const uint8_t *g = yf_prev + ((int64_t)(r & (YRp - 1)) * M + i) * PAIR + lane * REC_BYTES;
         f.y[2 * i] = gl8(g);
         f.y[2 * i + 1] = gl8(g + 8);
       }
     };
     auto fetch_z = [&](int32_t rz, Fetch &f) {  // z record rz (lanes 0 .. 2NW-1)
-      const uint8_t *g = zf_prev + (int64_t)(rz & (ZR - 1)) * ZREC + (lane & (2 * NW - 1)) * 16;
+      const uint8_t *g = zf_prev + (int64_t)(rz & (ZRp - 1)) * ZREC + (lane & (2 * NW - 1)) * 16;
       f.z[0] = gl8(g);
       f.z[1] = gl8(g + 8);
     };
@@ -847,11 +879,11 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
 #if defined(TSA_DIAG)
           lag_y = max(lag_y, t - prog_decode(lds_word(bpw)));
 #endif
-          wait_consumer(cons_y, seen_y, bpw, t - YR - YOFF + 1);
+          wait_consumer(cons_y, seen_y, bpw, t - YRm - YOFF + 1);
           const uint32_t tg = lap_tag(epoch, t);
 #pragma unroll
           for (int i = 0; i < M; ++i)
-            store16_sc1<SYS>(yf_mine + ((int64_t)(t & (YR - 1)) * M + i) * PAIR + lane * REC_BYTES,
+            store16_sc1<SYS>(yf_mine + ((int64_t)(t & (YRm - 1)) * M + i) * PAIR + lane * REC_BYTES,
                         make_uint4(perm(oIxy[i], oIy[i], 0x07060302u), tg,
                                    perm(oBest[i], oIyz[i], 0x07060302u), tg));
         }
@@ -871,10 +903,10 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
 #if defined(TSA_DIAG)
         lag_z = max(lag_z, t - prog_decode(lds_word(bpw + 1)));
 #endif
-        wait_consumer(cons_z, seen_z, bpw + 1, t - ZR - ZT - ZA + 1);
+        wait_consumer(cons_z, seen_z, bpw + 1, t - ZRm - ZT - ZA + 1);
         if (lane == 63) {
           const uint32_t tg = lap_tag(epoch, t);
-          uint8_t *zdst = zf_mine + (int64_t)(t & (ZR - 1)) * ZREC + w * LAP_ZREC_WAVE;
+          uint8_t *zdst = zf_mine + (int64_t)(t & (ZRm - 1)) * ZREC + w * LAP_ZREC_WAVE;
           store16_sc1<SYS>(zdst, make_uint4(oIz[M - 1], tg, oIxz[M - 1], tg));
           store16_sc1<SYS>(zdst + 16, make_uint4(Ryz[M - 1], tg, Rb[M - 1], tg));
         }
@@ -1014,16 +1046,19 @@ static DevInfo dev_info() {
   return cache[d];
 }
 
-// The SGPR bound on lap workgroups per CU: waves per SIMD the SGPR file admits
-// (build-time kernel table, kernel_meta.h), a workgroup of NW + 1 waves taking
-// up to ceil((NW + 1) / 4) of them on one SIMD -- the margin the guide asks for
-// near the occupancy API's SGPR edge (MI355X_MICROARCH.md:463).
-int lap_sgpr_blocks_per_cu(int M, int NW, bool f16, bool sop) {
+// The register bound on lap workgroups per CU: waves per SIMD the SGPR and
+// VGPR files admit (build-time kernel table, kernel_meta.h), a workgroup of
+// NW + 1 waves taking up to ceil((NW + 1) / 4) of them on one SIMD. The
+// occupancy API counts waves per CU instead and reads one workgroup high at
+// the SGPR edge (MI355X_MICROARCH.md:463) and, measured, at 96 VGPRs with
+// 9-wave workgroups (it said 2, the CU ran 1).
+int lap_simd_blocks_per_cu(int M, int NW, bool f16, bool sop) {
   char prefix[64];
   snprintf(prefix, sizeof prefix, "_ZN3tsa10lap_kernelILi%dELi%dELb%dELb%dELb0E", M, NW, f16 ? 1 : 0,
            sop ? 1 : 0);
-  const int sgpr = kernel_sgpr_max(prefix);
-  return sgpr_waves_per_simd(sgpr < 0 ? 112 : sgpr) / ((NW + 1 + 3) / 4);
+  const int sgpr = kernel_sgpr_max(prefix), vgpr = kernel_vgpr_max(prefix);
+  const int waves = std::min(sgpr_waves_per_simd(sgpr < 0 ? 112 : sgpr), vgpr_waves_per_simd(vgpr < 0 ? 256 : vgpr));
+  return waves / ((NW + 1 + 3) / 4);
 }
 // Workgroups of one instantiation a CU holds, from the HIP occupancy API on the
 // real kernel (VGPRs, LDS) capped by the SGPR bound (the API reads one block
@@ -1032,7 +1067,7 @@ template <int M, int NW, bool F16, bool SOP>
 static int lap_blocks_per_cu_t(size_t lds) {
   int nb = 0;
   int dev = -1;
-  const int sg = lap_sgpr_blocks_per_cu(M, NW, F16, SOP);
+  const int sg = lap_simd_blocks_per_cu(M, NW, F16, SOP);
   if (hipGetDevice(&dev) == hipSuccess &&
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lap_kernel<M, NW, F16, SOP, false>, 64 * (NW + 1),
                                                    lds) == hipSuccess)
@@ -1073,18 +1108,24 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   const int YOFF = 2 * (NW - 1) + 1;  // lap lag of a record (kernel: YOFF)
   const int32_t T = max_la + YOFF + ZT;  // >= every workgroup's step count
   auto pow2 = [](int64_t v) { int64_t p = 1; while (p < v) p <<= 1; return (int32_t)p; };
-  // ring slots beyond the natural lag: beyond 512 per side the lag between
-  // neighbours drifts further (more laps and tiles behind them) and 48 slots
-  // made producers wait (1024^3: 1235 back-pressure waits, 3.30 ms; 240 slots:
-  // 34 waits, 3.06 ms, 580 MB). A/B knob TSA_LAP_RING_SLACK.
-  int slack = std::max(max_la, std::max(max_lb, max_lc)) > 512 ? 240 : 48;
+  g.lds = lap_lds_bytes(M, NW, max_la);
+  const int64_t wgs = (int64_t)n * g.G * g.GZ;
+  const int per_cu = (g.lds > LDS_MAX) ? 0 : TSA_LAP_SHAPES(lap_blocks_per_cu_t, M, NW, f16, sop, g.lds);
+  const int cus = dev_info().cus;
+  // Slim rings: the lag between co-resident neighbours stays small (ring-lag
+  // census, TSA_DIAG, profiles/r3e_lap_lag.jsonl): y <= 55 steps, z <= 207
+  // beyond the natural ZT + ZA with one workgroup per CU; ~100 / ~200 with two
+  // sharing a CU. So 32 (one per CU) or 96 slots beyond the natural lag,
+  // rounded up to a power of 2. The big lags of round 2 (its workgroups start
+  // as round-1 ones finish: 671 steps at 1024^3) go to the boundary rings.
+  // A/B knob TSA_LAP_RING_SLACK (TSA_DIAG builds).
+  int slack = (per_cu >= 2 && wgs > cus) ? 96 : 32;
 #if defined(TSA_DIAG)
   if (const char *e = getenv("TSA_LAP_RING_SLACK")) slack = std::max(16, atoi(e));
 #endif
   g.YR = full_rings ? pow2(T) : pow2(YOFF + LPD + slack);
   g.ZR = full_rings ? pow2(T) : pow2(ZT + LPD + slack);
-  g.lds = lap_lds_bytes(M, NW, max_la);
-  const int64_t wgs = (int64_t)n * g.G * g.GZ;
+  g.YRB = g.ZRB = pow2(T);
   g.blocks = (int64_t)g.G * g.CH * 8;
   // progress words, the error word (+63 spare), the checked kernel's monitor (2 n)
   g.prog_bytes = (((size_t)wgs * LAP_PROG_STRIDE + 64 + 2 * (size_t)n) * sizeof(int32_t) + 255) &
@@ -1092,15 +1133,28 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   g.yf_bytes = (size_t)wgs * g.YR * M * 1024;
   g.zf_bytes = (size_t)wgs * g.ZR * NW * LAP_ZREC_WAVE;
   if (g.lds > LDS_MAX || g.blocks > 0x7FFFFFFF) return g;
-  const int per_cu = TSA_LAP_SHAPES(lap_blocks_per_cu_t, M, NW, f16, sop, g.lds);
-  const int cus = dev_info().cus;
-  // residency per XCD: column c (all its laps) lands on XCD c % 8
+  // residency per XCD: block b runs on XCD b % 8 (column c's laps on XCD
+  // c % 8), in block order, SX at a time (measured: tools/lap_trace.py xcc and
+  // start stamps)
   const int64_t wg_per_xcd = (int64_t)g.G * g.CH;
   const int64_t slots_xcd = (int64_t)std::max(1, cus / 8) * per_cu;
   g.per_cu = per_cu;
-  g.waves = per_cu > 0 ? std::max<int64_t>((wg_per_xcd + slots_xcd - 1) / slots_xcd,
-                                           (wgs + (int64_t)cus * per_cu - 1) / ((int64_t)cus * per_cu))
-                       : 0;
+  g.waves = per_cu > 0 ? (wg_per_xcd + slots_xcd - 1) / slots_xcd : 0;
+  // dispatch rounds: boundary rings for producers whose consumer is in a later
+  // round (kernel: y_bidx / z_bidx); one round, or full rings: none
+  g.SX = (full_rings || g.waves <= 1 || per_cu <= 0) ? (1 << 30) : (int32_t)slots_xcd;
+  g.KBY = g.KBZ = 0;
+  if (g.SX < (1 << 30)) {
+    if (g.CH >= g.SX) {
+      g.KBY = g.G;
+    } else {
+      for (int32_t c = 0; c < g.CH; ++c)
+        g.KBY = std::max(g.KBY, ((g.G - 1) * g.CH + c) / g.SX - c / g.SX);
+    }
+    g.KBZ = (int32_t)g.waves;  // index: the producer's round (< rounds)
+  }
+  g.yb_bytes = (size_t)g.NC * g.KBY * g.YRB * M * 1024;
+  g.zb_bytes = (size_t)g.KBZ * g.ZRB * NW * LAP_ZREC_WAVE;
   // one workgroup is the helix's job; a TSA_DIAG build allows it with
   // TSA_LAP_SINGLE=1 (the step time with no hand-off)
 #if defined(TSA_DIAG)
@@ -1111,18 +1165,25 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   g.ok = per_cu > 0 && (g.G >= 2 || g.GZ >= 2 || single);
   // estimated latency (us): the chain to the final workgroup -- each lap adds
   // YOFF + LPD + ~3 steps, each tile ZT + LPD + ~2 -- plus its own steps;
-  // several workgroups on one CU share its SIMDs. A grid beyond the resident
-  // slots runs in dispatch waves that barely overlap (~2.8x per wave).
+  // several workgroups on one CU share its SIMDs.
   const int64_t xcd_cus = std::max(1, cus / 8);
   const int64_t wg_cu = std::max<int64_t>(1, std::min<int64_t>(per_cu, (wg_per_xcd + xcd_cus - 1) / xcd_cus));
   const double steps = (double)(g.G - 1) * (YOFF + LPD + 3) + (double)(g.GZ - 1) * (ZT + LPD + 2) +
                        (double)(max_la + YOFF + ZT);
   const double chain = steps * lap_step_us(M, NW, wg_cu);
-  g.est_us = g.waves <= 1 ? chain : 2.8 * (double)g.waves * chain;
+  // a later round starts as the earlier one's workgroups finish: 1024^3 (M = 2,
+  // two rounds of one workgroup per CU) runs 3.04 ms against a 2.25 ms chain
+  g.est_us = chain * (1.0 + 0.35 * (double)(std::max<int64_t>(g.waves, 1) - 1));
   return g;
 }
 
-size_t lap_workspace_bytes(const LapGeom &g) { return g.prog_bytes + g.yf_bytes + g.zf_bytes; }
+size_t lap_workspace_bytes(const LapGeom &g) {
+  return g.prog_bytes + g.yf_bytes + g.zf_bytes + g.yb_bytes + g.zb_bytes;
+}
+static LapRounds lap_rounds(const LapGeom &g, void *d_ws) {
+  uint8_t *yb = (uint8_t *)d_ws + g.prog_bytes + g.yf_bytes + g.zf_bytes;
+  return LapRounds{g.SX, g.KBY, g.YRB, g.ZRB, yb, yb + g.yb_bytes};
+}
 uint32_t *lap_err_word(const LapGeom &g, int32_t n, void *d_ws) {
   return (uint32_t *)((int32_t *)d_ws + (int64_t)n * g.G * g.GZ * LAP_PROG_STRIDE);
 }
@@ -1165,7 +1226,8 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
     return TSA_EDEVICE;
   const uint32_t epoch = lap_next_epoch();
   hipLaunchKernelGGL(kfn, dim3((uint32_t)g.blocks), dim3(64 * (NW + 1)), g.lds, stream, d_seqs,
-                     d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, prog, err, d_scores, mon, pa,
+                     d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, lap_rounds(g, d_ws), prog, err,
+                     d_scores, mon, pa,
                      epoch, lap_spin_limit(), 0, g.G, yf, prog, trace);
   if (chk) {
     if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
@@ -1238,7 +1300,8 @@ static int launch_lap_split(const LapGeom &g, const PencilArgs &pa, const LapPar
     int32_t *prog_in = p > 0 ? (int32_t *)parts[p - 1].d_ws : prog;
     const int64_t blocks = (int64_t)(q.L1 - q.L0) * g.CH * 8;
     hipLaunchKernelGGL(kfn, dim3((uint32_t)blocks), dim3(64 * (NW + 1)), g.lds, q.stream, q.d_seqs,
-                       q.d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, prog, d_err, d_score,
+                       q.d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, lap_rounds(g, q.d_ws), prog,
+                       d_err, d_score,
                        (int32_t *)nullptr, pa, epoch, spin, q.L0, q.L1, yf_out, prog_in,
                        (unsigned long long *)nullptr);
     if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;

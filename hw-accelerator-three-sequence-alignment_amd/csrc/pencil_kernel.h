@@ -17,11 +17,11 @@ bool pencil_supported(const tsa_params *p);
 bool pencil_shape_supported(int32_t max_la, int32_t max_lb, int32_t max_lc);
 // Which single-cube (lap) schedules a launch may use:
 //   LAP_OFF      -- helix only (no cross-workgroup dependency at all);
-//   LAP_RESIDENT -- the lap kernel when its whole grid is co-resident;
-//   LAP_STREAM   -- also grids beyond the resident slots (relies on in-order
-//                   block dispatch; the caller must check *d_err after the
-//                   launch and rescore with LAP_OFF when it is set).
-// A lap launch that times out reports TSA_SCORE_INVALID for its triples.
+//   LAP_RESIDENT -- the lap kernel (async path);
+//   LAP_STREAM   -- the same plans on the synchronous paths, which check
+//                   *d_err after the launch and rescore with LAP_OFF.
+// Both run grids of up to LAP_MAX_WAVES dispatch rounds with boundary rings
+// (lap_geom); a lap launch that times out reports TSA_SCORE_INVALID.
 enum LapPolicy { LAP_OFF = 0, LAP_RESIDENT = 1, LAP_STREAM = 2 };
 // Certification limits of the checked kernel (DESIGN.md 1.2 with the observed
 // range of best in place of the a-priori one): a triple's scores stand when

@@ -133,12 +133,13 @@ static double helix_est(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_l
 
 // The lap kernel's geometry if it should run, else .ok = false (helix).
 // Resident grids (waves == 1) are safe: every workgroup runs at once, so a
-// consumer waiting for a record never holds a slot its producer needs. With
-// LAP_STREAM the grid may exceed the resident slots: producers always have
+// consumer waiting for a record never holds a slot its producer needs. A grid
+// beyond the resident slots runs in dispatch rounds: producers always have
 // lower block indices than their consumers, so with blocks dispatched in order
-// (observed, not promised by HIP) a consumer's producer is running or done;
-// the rings are then full length (no producer ever waits for a consumer), the
-// waits are bounded and the caller checks the error word and falls back.
+// per XCD (observed at 768^3 / 1024^3, where the M = 2 grid has always run
+// two rounds of one workgroup per CU; not promised by HIP) a consumer's
+// producer is running or done, and a producer never waits for a consumer of
+// a later round (boundary rings, lap_geom); every wait is bounded.
 static LapGeom lap_choice(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
                           LapPolicy lap, bool f16, bool sop, bool need = false) {
   LapGeom none{};
@@ -153,12 +154,16 @@ static LapGeom lap_choice(int32_t n, int32_t max_la, int32_t max_lb, int32_t max
   LapGeom best = none;
   for (int M = m_lo; M <= m_hi; M *= 2) {
     for (int NW = nw_lo; NW <= nw_hi; NW *= 2) {
-      LapGeom g = lap_geom(n, max_la, max_lb, max_lc, M, NW, false, f16, sop);
-      if (g.ok && g.waves > 1) {
-        if (lap != LAP_STREAM) continue;
-        g = lap_geom(n, max_la, max_lb, max_lc, M, NW, true, f16, sop);
-      }
+      // a grid of several dispatch rounds runs with boundary rings (lap_geom)
+      // on both paths: it relies on per-XCD in-order dispatch, measured
+      // (DESIGN.md 4.4); a hand-off that times out still reports, never hangs
+      const LapGeom g = lap_geom(n, max_la, max_lb, max_lc, M, NW, false, f16, sop);
       if (!g.ok || g.waves > LAP_MAX_WAVES) continue;
+      // rounds with two workgroups per CU: a later round's workgroups start out
+      // of chain order as slots free, lags reach ~1100 steps and the slim rings
+      // stall (1024^3 M = 1 NW = 8: 37206 back-pressure waits, timed out);
+      // with one per CU they start in chain order (M = 2: none, 3.00 ms)
+      if (g.waves > 1 && g.per_cu > 1) continue;
       if (!best.ok || g.est_us < best.est_us) best = g;
     }
   }

@@ -299,15 +299,15 @@ def test_pencil_lap_mode_small_batch(gpu, orc):
 
 def test_pencil_lap_streaming_batch(gpu, orc, monkeypatch, tmp_path):
     # sync batch API with more lap workgroups than resident slots: the grid runs
-    # in 2-3 dispatch waves (bounded spins, error word checked, helix rerun on
-    # timeout); 100 triples x 8 laps = 800 workgroups for 512 slots. The lap
-    # trace proves the streaming grid ran.
+    # in 2-3 dispatch rounds with boundary rings (bounded spins, error word
+    # checked, helix rerun on timeout); 60 triples x 8 laps x 2 tiles = 960
+    # workgroups (M = 1, NW = 8) for 512 slots. The lap trace proves it ran.
     monkeypatch.setenv("TSA_PENCIL_MODE", "lap")
     trace = tmp_path / "lap.csv"
     monkeypatch.setenv("TSA_LAP_TRACE", str(trace))
     rng = np.random.default_rng(91)
     triples = []
-    for _ in range(100):
+    for _ in range(60):
         la, lc = int(rng.integers(100, 129)), int(rng.integers(1, 129))
         triples.append(tuple(rng.integers(0, 4, n).astype(np.uint8) for n in (la, 128, lc)))
     seqs, offs = gpu.pack_batch(triples)

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("specs", nargs="+")
     ap.add_argument("--bits", type=int, default=12)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--kernel", default="pencil", help="pencil, or checked (the lap kernel with the range monitor)")
     args = ap.parse_args()
     import torch
     import bench
@@ -64,13 +65,13 @@ def main():
             seqs, offs = tsa.pack_batch([(a, b, c)])
             d_seqs, d_offs = torch.from_numpy(seqs).cuda(), torch.from_numpy(offs).cuda()
             d_sc = torch.zeros(1, dtype=torch.int32, device="cuda")
-            ws = tsa.workspace_size(1, la, lb, lc, p, "pencil")
+            ws = tsa.workspace_size(1, la, lb, lc, p, args.kernel)
             d_ws = torch.empty(max(ws, 16), dtype=torch.uint8, device="cuda")
             st = torch.cuda.current_stream()
 
             def call():
                 tsa.score_batch_async(d_seqs.data_ptr(), d_offs.data_ptr(), 1, la, lb, lc,
-                                      d_sc.data_ptr(), d_ws.data_ptr(), ws, st.cuda_stream, p, "pencil")
+                                      d_sc.data_ptr(), d_ws.data_ptr(), ws, st.cuda_stream, p, args.kernel)
             call()
             torch.cuda.synchronize()
             times = []
@@ -82,7 +83,7 @@ def main():
                 torch.cuda.synchronize()
                 times.append(e0.elapsed_time(e1) * 1e3)
             score = int(d_sc.item())
-            plan = tsa.describe_plan(1, la, lb, lc, p, kernel="pencil", sync=False)
+            plan = tsa.describe_plan(1, la, lb, lc, p, kernel=args.kernel, sync=False)
             path = os.path.join(out_dir, "lap_trace_" + re.sub(r"[^0-9A-Za-z_=.-]", "_", spec) + ".csv")
             os.environ["TSA_LAP_TRACE"] = path
             call()
