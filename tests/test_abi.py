@@ -137,6 +137,23 @@ def test_describe_plan(tsa):
     assert tsa.describe_plan(4096, 800, 800, 800, p, sync=True) == "plane"
 
 
+def test_lap_rounds_and_ring_memory(tsa):
+    """The M = 2 lap grid of a 1024^3 cube holds one workgroup per CU (per-SIMD
+    register model), so it runs two dispatch rounds with boundary rings; the
+    O(N^2) workspace stays within 150 MB (round 2: 580 MB). Host-only."""
+    p16 = tsa.TsaParams.default(score_bits=16)
+    plan = tsa.describe_plan(1, 1024, 1024, 1024, p16, sync=False)
+    assert plan.startswith("pencil lap i16 rtl M=2 NW=8") and "waves=2" in plan, plan
+    assert tsa.workspace_size(1, 1024, 1024, 1024, p16, "pencil") <= 150e6
+    # within one round: slim rings only (no boundary ring memory)
+    p = tsa.TsaParams.default()
+    assert "waves=1" in tsa.describe_plan(1, 512, 512, 512, p, sync=False)
+    assert tsa.workspace_size(1, 512, 512, 512, p, "pencil") <= 30e6
+    # O(N^2): 256^3 -> 512^3 grows ~4x at most
+    w256 = tsa.workspace_size(1, 256, 256, 256, p, "pencil")
+    assert tsa.workspace_size(1, 512, 512, 512, p, "pencil") / w256 < 4.5
+
+
 @pytest.mark.skipif(os.environ.get("TSA_EXPECT_GPU") == "1", reason="GPU box")
 def test_no_cpu_fallback_without_gpu(tsa):
     if tsa.device_count() > 0:
