@@ -42,7 +42,9 @@ struct LitArgs {
   int32_t sh, packed;
 };
 
-constexpr int LIT_NW = 8, LIT_S = 2, LIT_PD = 8, LIT_RING_EXTRA = 8;
+constexpr int LIT_NW = 8, LIT_S = 2, LIT_RING_EXTRA = 8;
+// ring rows wave 0 prefetches (LDS-DMA): 8, 4 at M = 4 (LDS)
+__host__ __device__ constexpr int lit_pd(int M) { return M >= 4 ? 4 : 8; }
 
 struct LitGeom {
   int32_t M, P, R;
@@ -51,18 +53,18 @@ struct LitGeom {
 };
 static LitGeom lit_geom(int32_t max_la, int32_t max_lb, int32_t max_lc) {
   LitGeom g;
-  g.M = max_lc <= 128 ? 1 : 2;
+  g.M = max_lc <= 128 ? 1 : max_lc <= 256 ? 2 : 4;
   g.P = std::max(max_la + 1, 128 * g.M);  // x' = 0 .. LA: the face column first
   g.P = (g.P + g.M - 1) / g.M * g.M;       // M = 2: the x' = 0 register is (t - w) parity
   g.R = g.P + LIT_RING_EXTRA;
   g.ring_bytes_per_triple = (int64_t)g.R * g.M * 64 * REC_BYTES;
-  g.lds = (size_t)(LIT_NW - 1) * 2 * LIT_S * g.M * 1024 + (size_t)LIT_PD * g.M * 1024 +
+  g.lds = (size_t)(LIT_NW - 1) * 2 * LIT_S * g.M * 1024 + (size_t)lit_pd(g.M) * g.M * 1024 +
           4 * ((size_t)g.P + 128 * g.M) + 4 * (((size_t)max_lb + 4) & ~(size_t)3) + (size_t)7 * g.M * 256 + 32;
   return g;
 }
 
 bool literal_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc) {
-  if (max_la < 1 || max_lb < 1 || max_lc < 1 || max_lc > 256 || max_la > 4095 || max_lb > 4096) return false;
+  if (max_la < 1 || max_lb < 1 || max_lc < 1 || max_lc > 512 || max_la > 4095 || max_lb > 4096) return false;
   return lit_geom(max_la, max_lb, max_lc).lds <= LDS_MAX;
 }
 bool literal_helix_chosen(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
@@ -78,8 +80,10 @@ bool literal_helix_chosen(int32_t n, int32_t max_la, int32_t max_lb, int32_t max
   // (y,z) cells. A few large cubes sweep faster as planes over the chip.
   const LitGeom g = lit_geom(max_la, max_lb, max_lc);
   const double T = (double)((max_lb + LIT_NW - 1) / LIT_NW) * g.P + LIT_S * (LIT_NW - 1) + max_lc;
-  const double waves = n > 256 ? 1.8 * (double)((n + 511) / 512) : 1.0;
-  const double lit_us = T * (g.M == 1 ? 0.56 : 0.95) * waves;
+  // M = 4 (208 VGPRs) runs one workgroup per CU: ~2x the M = 2 step (an estimate)
+  const double waves = g.M == 4 ? (double)((n + 255) / 256)
+                                : n > 256 ? 1.8 * (double)((n + 511) / 512) : 1.0;
+  const double lit_us = T * (g.M == 1 ? 0.56 : g.M == 2 ? 0.95 : 1.9) * waves;
   const double plane_us = (double)(max_la + max_lb + max_lc) *
                           (4.4 + 0.41 * (double)n * (double)max_lb * (double)max_lc / 65536.0);
   return lit_us <= plane_us;
@@ -144,7 +148,7 @@ __global__ __launch_bounds__(64 * LIT_NW) void literal_kernel(
     int32_t lds_a, int32_t lds_b, int64_t ring_stride, uint8_t *__restrict__ ring_base,
     int32_t *__restrict__ scores, int32_t *__restrict__ final7, LitArgs ca) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  constexpr int NW = LIT_NW, S = LIT_S, PD = LIT_PD, ZT = 128 * M;
+  constexpr int NW = LIT_NW, S = LIT_S, PD = lit_pd(M), ZT = 128 * M;
   constexpr int PAIR_BYTES = 64 * REC_BYTES, SLOT_BYTES = M * PAIR_BYTES;
   uint8_t *xr = smem;
   uint8_t *xr0 = xr + (NW - 1) * 4 * SLOT_BYTES;
@@ -517,6 +521,9 @@ int literal_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_
   if (g.M == 1)
     return sop ? launch_lit<1, true>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_final7, d_ws, ca, stream)
                : launch_lit<1, false>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_final7, d_ws, ca, stream);
+  if (g.M == 4)
+    return sop ? launch_lit<4, true>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_final7, d_ws, ca, stream)
+               : launch_lit<4, false>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_final7, d_ws, ca, stream);
   return sop ? launch_lit<2, true>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_final7, d_ws, ca, stream)
              : launch_lit<2, false>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_final7, d_ws, ca, stream);
 }

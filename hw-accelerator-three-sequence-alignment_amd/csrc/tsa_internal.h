@@ -65,7 +65,7 @@ int plane_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t 
                        int32_t *d_scores, int32_t *d_final7, void *d_ws, size_t ws_bytes,
                        hipStream_t stream, uint32_t *d_tb = nullptr);
 // ---- literal helix (literal_kernel.hip): TSA_KERNEL_PLANE's batch path -----
-// The RTL's literal arithmetic in push form on the helix schedule, LC <= 256.
+// The RTL's literal arithmetic in push form on the helix schedule, LC <= 512.
 bool literal_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc);
 size_t literal_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc);
 int literal_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, int32_t max_la,

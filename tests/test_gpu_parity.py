@@ -706,11 +706,11 @@ def test_literal_helix_matches_oracle(gpu, orc, monkeypatch, bits, s3_mode):
     """The RTL's literal arithmetic in push form on the helix schedule (every
     candidate wrapped to SCORE_BITS by int16 arithmetic on values shifted left
     by 16 - SCORE_BITS; tools/literal_emu.py replays it): narrow words that
-    wrap, both s3 modes, ragged batches over M = 1 and 2, related triples."""
+    wrap, both s3 modes, ragged batches over M = 1, 2 and 4, related triples."""
     monkeypatch.setenv("TSA_PENCIL_MODE", "literal")
     rng = np.random.default_rng(200 + bits + s3_mode)
     p, op = gpu.TsaParams.default(score_bits=bits, s3_mode=s3_mode), orc.default_params(score_bits=bits, s3_mode=s3_mode)
-    for n, hi in ((7, (150, 30, 100)), (5, (260, 21, 256)), (3, (40, 17, 129))):
+    for n, hi in ((7, (150, 30, 100)), (5, (260, 21, 256)), (3, (40, 17, 129)), (3, (90, 12, 512))):
         triples = [tuple(rng.integers(0, 5, int(rng.integers(1, h + 1))).astype(np.uint8) for h in hi)
                    for _ in range(n)]
         a = rng.integers(0, 4, 120).astype(np.uint8)

@@ -47,7 +47,8 @@ def test_emulated_vspace_lam2(orc):
 
 
 @pytest.mark.parametrize("la,lb,lc,sop,bits", [(8, 8, 8, 0, 12), (20, 9, 30, 0, 12), (47, 17, 128, 1, 12),
-                                               (60, 3, 130, 0, 12), (30, 20, 40, 0, 5), (25, 17, 33, 1, 4)])
+                                               (60, 3, 130, 0, 12), (30, 20, 40, 0, 5), (25, 17, 33, 1, 4),
+                                               (4, 2, 260, 0, 6)])
 def test_emulated_literal_helix(orc, la, lb, lc, sop, bits):
     """tools/literal_emu.py: the literal push form on the helix schedule (the
     x = 0 face column, row 0's pushes in the ring, the z = 0 pushes of a zero

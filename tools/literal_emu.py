@@ -44,7 +44,7 @@ def penalties(go, ge):
 def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, bits=12):
     """(score, final7) of one triple by the literal helix schedule."""
     la, lb, lc = len(a), len(b), len(c)
-    M = 1 if lc <= 128 else 2
+    M = 1 if lc <= 128 else 2 if lc <= 256 else 4
     KS = 128 * M
     P = max(la + 1, KS)
     P = -(-P // M) * M
