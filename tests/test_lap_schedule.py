@@ -64,3 +64,20 @@ def test_lap_split_cell_algebra():
         got = (max(Y, W), max(Y - OE, N[0]), max(Y - E2, N[1]), max(Y - OE, N[2]),
                max(Y - E, N[3]), max(Y - E, N[4]), max(Y - O, N[5]))
         assert got == ref
+
+
+@pytest.mark.parametrize("shape,kw", [((20, 11, 70), {}), ((25, 17, 33), {"sop": True}),
+                                      ((30, 20, 40), {"bits": 5}), ((40, 19, 70), {"NW": 4}),
+                                      ((20, 9, 150), {"M": 2}), ((12, 30, 5), {"NW": 8})])
+def test_literal_lap_schedule_matches_oracle(orc, shape, kw):
+    """tools/litlap_emu.py: the lap schedule with the literal push-form cell
+    (x' = 0 face column, step-varying y = 0 / z = 0 faces of zero cells,
+    successor symbols, wrapped candidates) equals the literal oracle, final
+    7-tuple included, over laps, tiles, NW and M."""
+    import litlap_emu
+    rng = np.random.default_rng(sum(shape))
+    a, b, c = (rng.integers(0, 5, n) for n in shape)
+    got = litlap_emu.emulate(a, b, c, **kw)
+    p = orc.default_params(s3_mode=int(kw.get("sop", False)), score_bits=kw.get("bits", 12))
+    s, fin = orc.score(a, b, c, p, final_states=True)
+    assert (got[0], tuple(got[1])) == (s, tuple(fin))
