@@ -38,8 +38,9 @@ constexpr int64_t LAP_MAX_WAVES = 3;
 // Geometry of the lap schedule (M pairs per lane, NW waves) for a batch of n
 // triples; full_rings: every ring as long as the cube (no back-pressure: the
 // split over devices, whose parts may queue behind each other).
+// lit: the literal form (lap_kernel LIT: int16 shifted words, M <= 2).
 LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW,
-                 bool full_rings, bool f16, bool sop);
+                 bool full_rings, bool f16, bool sop, bool lit = false);
 size_t lap_workspace_bytes(const LapGeom &g);
 // The launch's error word inside a workspace of n triples (set on a hand-off timeout).
 uint32_t *lap_err_word(const LapGeom &g, int32_t n, void *d_ws);
@@ -51,6 +52,13 @@ int lap_launch(const LapGeom &g, bool f16, bool sop, const uint8_t *d_seqs,
                const int64_t *d_offsets, int32_t n, int32_t *d_scores, void *d_ws,
                const PencilArgs &pa, hipStream_t stream, int32_t **d_err,
                const CheckLimits *chk = nullptr);
+
+// The literal form on a geometry from lap_geom(..., lit = true): the RTL's
+// wrapped arithmetic for any parameter set; d_final7 (may be null) receives
+// each triple's final 7-tuple {M, Ix, Iy, Iz, Ixy, Iyz, Ixz}. d_err as above.
+int lap_launch_lit(const LapGeom &g, bool sop, const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
+                   int32_t *d_scores, int32_t *d_final7, void *d_ws, const KParams &kp, hipStream_t stream,
+                   int32_t **d_err);
 
 // One part of a single cube split over devices by laps (tsa_score_gpu_multi):
 // laps [L0, L1) on `device`, with that device's copy of the triple and a

@@ -91,12 +91,19 @@ __host__ __device__ __forceinline__ uint32_t lap_tag(uint32_t e, int32_t s) {
   return e ^ ((uint32_t)s * 0x9E3779B1u);
 }
 
-static size_t lap_lds_bytes(int M, int NW, int32_t max_la) {
-  const int ZT = 64 * M, SLOT = M * 1024;
+// A code pairs the table holds: the LIT loader reads a few entries further
+// (its z = 0 faces run ZA steps ahead of the last compute step)
+__host__ __device__ constexpr int32_t lap_na(int32_t la, int M, int NW, bool lit) {
+  return la + 2 * 64 * M + 4 * NW + 8 + (lit ? 2 * NW + 8 : 0);
+}
+// final-cell words: best of the final step, or (LIT) its 7 input states + 8
+__host__ __device__ constexpr int lap_fin_words(int M, bool lit) { return lit ? 7 * M * 64 + 8 : M * 64; }
+static size_t lap_lds_bytes(int M, int NW, int32_t max_la, bool lit = false) {
+  const int SLOT = M * 1024;
   return (size_t)(NW - 1) * lap_k(M) * SLOT + (size_t)lap_k0(M) * SLOT +
          (size_t)LAP_ZL * NW * LAP_ZREC_WAVE + (size_t)SLOT + (size_t)NW * LAP_ZREC_WAVE + 16 * 4 +
-         (size_t)(NW + 1) * 256 + (size_t)M * 256 +
-         4 * (((size_t)max_la + 2 * ZT + 4 * NW + 8 + 3) & ~(size_t)3);
+         (size_t)(NW + 1) * 256 + (size_t)lap_fin_words(M, lit) * 4 +
+         4 * (((size_t)lap_na(max_la, M, NW, lit) + 3) & ~(size_t)3);
 }
 
 // Trace slots per block (TSA_LAP_TRACE): 8, plus with TSA_DIAG (the
@@ -288,6 +295,88 @@ __device__ __forceinline__ void lap_post_i16(const PencilArgs &pa, const uint32_
   }
 }
 
+// LIT: the literal push-form cell (literal_kernel.hip:push_literal, the RTL's
+// src/PE_1cyc.v:164-218 with every candidate wrapped at SCORE_BITS), split at
+// the row above the same way: every candidate but Y's is maxed before the
+// record lands, Y's seven after it (13 instructions per pair). an / bn / cn:
+// the successors' symbol codes (a_{x'+1}, b_{y+1}, c_{z+1}); UYZ = s2(b_{y+1},
+// c_{z+1}) - GE and K1 (the [b=c] part of s3) are per-position constants.
+template <int M>
+struct LitPre {
+  uint32_t pIx[M], pIy[M], pIz[M], pIxy[M], pIyz[M], pIxz[M], pM[M], uxy[M], vxz[M], s3[M];
+};
+template <int M, bool SOP>
+__device__ __forceinline__ void lit_pre(const LitArgs &c, const LitArgs &cv, uint32_t ones,
+                                        const uint32_t (&an)[M], uint32_t bn, const uint32_t (&cn)[M],
+                                        const uint32_t (&UYZ)[M], const uint32_t (&K1)[M],
+                                        const uint32_t (&X)[M], const uint32_t (&Z)[M],
+                                        const uint32_t (&XY)[M], const uint32_t (&YZ)[M],
+                                        const uint32_t (&XZ)[M], const uint32_t (&MM)[M], LitPre<M> &p) {
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    // single targets, less Y's candidates (src/PE_1cyc.v:172-194)
+    const uint32_t m2O = pk_add(MM[i], c.n2O);
+    const uint32_t x2E = pk_add(X[i], c.n2E), xOE = pk_add(X[i], c.nOE);
+    const uint32_t z2E = pk_add(Z[i], c.n2E), zOE = pk_add(Z[i], c.nOE);
+    const uint32_t xyOE = pk_add(XY[i], c.nOE), xy2O = pk_add(XY[i], c.n2O);
+    const uint32_t yzOE = pk_add(YZ[i], c.nOE), yz2O = pk_add(YZ[i], c.n2O);
+    const uint32_t xzOE = pk_add(XZ[i], c.nOE), xz2O = pk_add(XZ[i], c.n2O);
+    const uint32_t A = pk_max(pk_max(m2O, zOE), xyOE), Bv = pk_max(xOE, yzOE);
+    p.pIx[i] = pk_max(pk_max(A, x2E), pk_max(yz2O, xzOE));
+    p.pIy[i] = pk_max(pk_max(A, Bv), xz2O);
+    p.pIz[i] = pk_max(pk_max(Bv, m2O), pk_max(z2E, pk_max(xy2O, xzOE)));
+    // the successors' pair scores less GE (u) and less GO (v), src/PE_1cyc.v:159-161
+    const uint32_t eab = pk_eq1(an[i], bn, ones), eac = pk_eq1(an[i], cn[i], ones);
+    const uint32_t uxy = pk_mad(eab, cv.dmS, cv.mmE), vxy = pk_add(uxy, c.nDOE);
+    const uint32_t uxz = pk_mad(eac, cv.dmS, cv.mmE), vxz = pk_add(uxz, c.nDOE);
+    const uint32_t uyz = UYZ[i], vyz = pk_add(uyz, c.nDOE);
+    p.pIxy[i] = pk_max(pk_max(pk_max(pk_add(X[i], uxy), pk_add(XY[i], uxy)), pk_max(pk_add(MM[i], vxy), pk_add(Z[i], vxy))),
+                       pk_max(pk_add(YZ[i], vxy), pk_add(XZ[i], vxy)));
+    p.pIyz[i] = pk_max(pk_max(pk_max(pk_add(Z[i], uyz), pk_add(YZ[i], uyz)), pk_max(pk_add(MM[i], vyz), pk_add(X[i], vyz))),
+                       pk_max(pk_add(XY[i], vyz), pk_add(XZ[i], vyz)));
+    p.pIxz[i] = pk_max(pk_max(pk_max(pk_add(X[i], uxz), pk_add(Z[i], uxz)), pk_max(pk_add(XZ[i], uxz), pk_add(MM[i], vxz))),
+                       pk_max(pk_add(XY[i], vxz), pk_add(YZ[i], vxz)));
+    // M: every state plus the successor's triple score (src/PE_1cyc.v:162-170)
+    uint32_t s3;
+    if constexpr (SOP) s3 = pk_mad(eab, cv.dmS, pk_mad(eac, cv.dmS, K1[i]));
+    else s3 = pk_mad(eab, K1[i], cv.neS);
+    p.pM[i] = pk_max(pk_max(pk_max(pk_add(MM[i], s3), pk_add(X[i], s3)), pk_max(pk_add(Z[i], s3), pk_add(XY[i], s3))),
+                     pk_max(pk_add(YZ[i], s3), pk_add(XZ[i], s3)));
+    p.uxy[i] = uxy;
+    p.vxz[i] = vxz;
+    p.s3[i] = s3;
+  }
+}
+template <int M>
+__device__ __forceinline__ void lit_post(const LitArgs &c, const uint32_t (&Y)[M], const uint32_t (&UYZ)[M],
+                                         const LitPre<M> &p, uint32_t (&nIx)[M], uint32_t (&oIy)[M],
+                                         uint32_t (&oIz)[M], uint32_t (&oIxy)[M], uint32_t (&oIyz)[M],
+                                         uint32_t (&oIxz)[M], uint32_t (&oM)[M]) {
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const uint32_t y = Y[i], yOE = pk_add(y, c.nOE);
+    nIx[i] = pk_max(p.pIx[i], yOE);
+    oIy[i] = pk_max(p.pIy[i], pk_add(y, c.n2E));
+    oIz[i] = pk_max(p.pIz[i], yOE);
+    oIxy[i] = pk_max(p.pIxy[i], pk_add(y, p.uxy[i]));
+    oIyz[i] = pk_max(p.pIyz[i], pk_add(y, UYZ[i]));
+    oIxz[i] = pk_max(p.pIxz[i], pk_add(y, p.vxz[i]));
+    oM[i] = pk_max(p.pM[i], pk_add(y, p.s3[i]));
+  }
+}
+// A zero cell's pushes (the faces) into a pair target and into M, per half:
+// s2 of the successor's pair as fP[0] / fP[1], and s3 wrapped (P[M][*] = 0)
+__device__ __forceinline__ uint32_t lit_face_pair(const LitArgs &cv, uint32_t p, uint32_t q, uint32_t ones) {
+  return pk_mad(pk_eq1(p, q, ones), pk_sub(cv.fP[1], cv.fP[0]), cv.fP[0]);
+}
+template <bool SOP>
+__device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, uint32_t bn, uint32_t cn,
+                                               uint32_t ones) {
+  const uint32_t eab = pk_eq1(an, bn, ones), ebc = pk_eq1(bn, cn, ones), eac = pk_eq1(an, cn, ones);
+  if constexpr (SOP) return pk_mad(eab, cv.dmS, pk_mad(ebc, cv.dmS, pk_mad(eac, cv.dmS, cv.mm3S)));
+  else return pk_mad(eab, pk_mad(ebc, cv.d1S, cv.d0S), cv.neS);
+}
+
 // LDS (bytes):
 //   xr    [NW-1][K][M][64][16]  wave w -> w+1 records {Iy, Ixy, Iyz, best}
 //   xr0   [K0][M][64][16]       tagged y records of the lap above (loader, LDS-DMA)
@@ -297,7 +386,8 @@ __device__ __forceinline__ void lap_post_i16(const PencilArgs &pa, const uint32_
 //   wd    [16] i32              [9] back-pressure waits, [12] abort, [13..14] the
 //                               consumers' progress (LDS-DMA'd), [15] loader stalls
 //   pw    [NW+1][64] i32        progress words (steps done): compute wave w, loader NW
-//   fin   [M][64] u32           best of the final step
+//   fin   [M][64] u32           best of the final step (LIT: [7][M][64] its input
+//                               states, then the 7 unshifted values)
 //   sA2   [..] u32              A code pairs: entry j = x j-OFF (lo), j-OFF-1 (hi)
 // Minimum waves per SIMD the register allocation must allow. A workgroup's
 // NW + 1 waves may sit ceil((NW + 1) / 4) to a SIMD (the dispatcher need not
@@ -308,7 +398,9 @@ __device__ __forceinline__ void lap_post_i16(const PencilArgs &pa, const uint32_
 #ifndef TSA_LAP_WPE2
 #define TSA_LAP_WPE2 5
 #endif
-__host__ __device__ constexpr int lap_waves_per_eu(int M) { return M == 1 ? 4 : M == 2 ? TSA_LAP_WPE2 : 2; }
+__host__ __device__ constexpr int lap_waves_per_eu(int M, bool lit = false) {
+  return lit ? (M == 1 ? 4 : 3) : M == 1 ? 4 : M == 2 ? TSA_LAP_WPE2 : 2;
+}
 // f(integral_constant<J>) for J = B .. E-1, unrolled at compile time
 template <int B, int E, class F>
 __device__ __forceinline__ void static_for(F &&f) {
@@ -333,18 +425,27 @@ __device__ __forceinline__ void static_for(F &&f) {
 // part's workspace (yf_out, its consumer's memory) and the progress words of
 // lap L0 into the previous part's (prog_in, its producer's memory), so every
 // poll reads local memory and only posted stores cross the link.
-template <int M, int NW, bool F16, bool SOP, bool CHK, bool SYS = false>
-__global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel(
+// LIT: the literal RTL arithmetic (tools/litlap_emu.py replays it): the push-
+// form cell of the literal helix on this schedule -- a position computes
+// x' = u (x' = 0 the x = 0 face: its 7 inputs forced to 0, one more step), it
+// pushes with its successors' symbols, the loader writes the y = 0 / z = 0
+// faces (zero cells pushing with the receivers' symbols, so they vary with the
+// step) into the rings wave 0 and position 0 read, values are shifted left by
+// 16 - SCORE_BITS so int16 adds wrap at the RTL word, and the final cell's 7
+// input states go to mon (aux) as its final 7-tuple.
+template <int M, int NW, bool F16, bool SOP, bool CHK, bool SYS = false, bool LIT = false>
+__global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_kernel(
     const uint8_t *__restrict__ seqs, const int64_t *__restrict__ offs, int32_t G, int32_t GZ,
     int32_t NC, int32_t CH, int32_t YR, int32_t ZR, uint8_t *__restrict__ yf_base,
     uint8_t *__restrict__ zf_base, LapRounds rd, int32_t *__restrict__ prog, uint32_t *__restrict__ err,
     int32_t *__restrict__ scores, int32_t *__restrict__ mon, PencilArgs pa, uint32_t epoch,
     uint32_t spin_limit, int32_t L0, int32_t L1, uint8_t *__restrict__ yf_out,
     int32_t *__restrict__ prog_in,
-    unsigned long long *__restrict__ trace) {
+    unsigned long long *__restrict__ trace, LitArgs lit) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   static_assert(!(CHK && F16), "the checked kernel runs the int16 form");
   static_assert(!(CHK && SYS), "a split cube runs the unchecked forms");
+  static_assert(!(LIT && (F16 || CHK || SYS)), "the literal form: int16, unchecked, one device");
   constexpr int SCOPE = SYS ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
   constexpr int RW = 2 * NW, ZT = 64 * M, LPD = lap_pd(M), K = lap_k(M), K0 = lap_k0(M);
   constexpr int PAIR = 64 * REC_BYTES, SLOT = M * PAIR;
@@ -361,7 +462,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
   int32_t *wd = (int32_t *)(zface + ZREC);
   int32_t *pw = wd + 16;
   uint32_t *fin = (uint32_t *)(pw + 64 * (NW + 1));
-  uint32_t *sA2 = fin + M * 64;
+  uint32_t *sA2 = fin + lap_fin_words(M, LIT);
   int32_t *const w_bp = wd + 9, *const w_abort = wd + 12, *const bpw = wd + 13, *const w_stall = wd + 15;
 
   const int lane = threadIdx.x & 63;
@@ -398,9 +499,10 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
   const bool final_wg = !yout && !zout;
   auto tau = [](int32_t r) { return 2 * (r >> 1) + (r & 1); };  // step offset of lap row r
   const int32_t r_f = lb - 1 - L * RW, k_f = lc - 1 - q * ZT;
-  const int32_t T = final_wg ? (la - 1) + tau(r_f) + k_f + 1 : la + tau(rows - 1) + zt_q - 1;
-  const int32_t T_above = la + tau(RW - 1) + zt_q - 1;  // records the lap above writes (same tile)
-  const int32_t T_left = la + tau(rows - 1) + ZT - 1;   // z records the tile to the left writes
+  constexpr int32_t LX = LIT ? 1 : 0;  // LIT: x' = 0 .. la, one step more
+  const int32_t T = final_wg ? (la - 1 + LX) + tau(r_f) + k_f + 1 : la + LX + tau(rows - 1) + zt_q - 1;
+  const int32_t T_above = la + LX + tau(RW - 1) + zt_q - 1;  // records the lap above writes (same tile)
+  const int32_t T_left = la + LX + tau(rows - 1) + ZT - 1;   // z records the tile to the left writes
   // Rings. A grid beyond the resident slots runs in dispatch rounds (per XCD,
   // in block order: rd.SX slots each). A producer whose consumer is in a later
   // round gets a full-length ring from the boundary region (it never waits
@@ -463,7 +565,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
   };
 
   // ---- A code pairs, zeroed words
-  const int32_t na = la + 2 * ZT + 4 * NW + 8;
+  const int32_t na = lap_na(la, M, NW, LIT);
   for (int j = threadIdx.x; j < na; j += 64 * (NW + 1)) {
     const int x0 = j - OFF, x1 = j - OFF - 1;
     const uint32_t c0 = (x0 >= 0 && x0 < la) ? SYM0 << tsa_sym(seqs, o0 + x0, pa.packed) : 0u;
@@ -523,6 +625,43 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       f.py = __hip_atomic_load(prog + cons_y * LAP_PROG_STRIDE, __ATOMIC_RELAXED, SCOPE);
       f.pz = __hip_atomic_load(prog + cons_z * LAP_PROG_STRIDE, __ATOMIC_RELAXED, SCOPE);
     };
+    // LIT: the y = 0 (lap 0) and z = 0 (tile 0) faces, written into the rings
+    // wave 0 and position 0 read: zero cells pushing with the receivers'
+    // symbols (tools/litlap_emu.py zero_push), so they vary with the step
+    uint32_t lones = 0x00010001u, lb1 = 0, lc1 = 0, lby2 = 0, lcn[M], lfyz[M];
+    LitArgs cv = lit;
+    if constexpr (LIT) {
+      asm volatile("" : "+v"(lones), "+v"(cv.dmS), "+v"(cv.d1S), "+v"(cv.d0S), "+v"(cv.neS), "+v"(cv.mm3S),
+                   "+v"(cv.fP[0]), "+v"(cv.fP[1]));
+      auto code = [&](int64_t base, int32_t i, int32_t len) -> uint32_t {
+        return (i >= 0 && i < len) ? SYM0 << tsa_sym(seqs, base + i, pa.packed) : 0u;
+      };
+      lb1 = code(o1, 0, lb) * 0x00010001u;  // b_1 (the y = 0 face is lap 0's)
+      lc1 = code(o2, 0, lc) * 0x00010001u;  // c_1
+      const int32_t yz = L * RW + 2 * ((lane & (2 * NW - 1)) >> 1);
+      lby2 = code(o1, yz, lb) | (code(o1, yz + 1, lb) << 16);  // b_y of the two rows of wave lane / 2
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        lcn[i] = code(o2, q * ZT + M * lane + i + 1, lc) * 0x00010001u;  // c_{z+1}
+        lfyz[i] = lit_face_pair(cv, lb1, lcn[i], lones);
+      }
+    }
+    // wave 0's record of step s: row 0's pushes into row 1 at x' = s - k, in
+    // the tagged record format (low halves: Iy | Ixy << 16, Iyz | M << 16)
+    auto yface_lit = [&](int32_t s, int i) -> uint4 {
+      const uint32_t an = sA2[s - (M * lane + i) + OFF] & 0xFFFFu;  // a_{x'+1}
+      const uint32_t fxy = lit_face_pair(cv, an, lb1, lones), fm = lit_face_m<SOP>(cv, an, lb1, lcn[i], lones);
+      return make_uint4((cv.fS[1] & 0xFFFFu) | (fxy << 16), 0u, (lfyz[i] & 0xFFFFu) | (fm << 16), 0u);
+    };
+    // z record rz (lanes 0 .. 2NW-1: wave lane / 2, word pair lane & 1): the
+    // z = 0 cells of that wave's two rows at x' = rz - ZT + 1 - 2w - h
+    auto zface_lit = [&](int32_t rz) -> uint4 {
+      const int32_t wz = (lane & (2 * NW - 1)) >> 1;
+      const uint32_t a2 = sA2[rz - ZT + 1 - 2 * wz + OFF];  // a_{x'+1}: row 2wz (lo), 2wz + 1 (hi)
+      if (lane & 1)
+        return make_uint4(lit_face_pair(cv, lby2, lc1, lones), 0u, lit_face_m<SOP>(cv, a2, lby2, lc1, lones), 0u);
+      return make_uint4(cv.fS[2], 0u, lit_face_pair(cv, a2, lc1, lones), 0u);
+    };
     auto tag_ok = [](u64 g, uint32_t tg) { return (uint32_t)(g >> 32) == tg; };
     auto y_ok = [&](int32_t s, const Fetch &f) {
       const uint32_t tg = lap_tag(epoch, s + YOFF);
@@ -565,20 +704,27 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
     // sees those cells too, and must not see stale ring contents)
     auto put_z = [&](int32_t rz, const Fetch &f) {
       const bool real = rz < T_left;
-      if (lane < 2 * NW)
-        lds_write16(zring + (rz & (LAP_ZL - 1)) * ZREC + lane * 16,
-                    real ? make_uint4((uint32_t)f.z[0], (uint32_t)(f.z[0] >> 32), (uint32_t)f.z[1],
-                                      (uint32_t)(f.z[1] >> 32))
-                         : make_uint4(0u, 0u, 0u, 0u));
+      if (lane < 2 * NW) {
+        uint4 v = real ? make_uint4((uint32_t)f.z[0], (uint32_t)(f.z[0] >> 32), (uint32_t)f.z[1],
+                                    (uint32_t)(f.z[1] >> 32))
+                       : make_uint4(0u, 0u, 0u, 0u);
+        if constexpr (LIT) {
+          if (!zin) v = zface_lit(rz);
+        }
+        lds_write16(zring + (rz & (LAP_ZL - 1)) * ZREC + lane * 16, v);
+      }
     };
     int32_t seen_w0 = 0, seen_wl = 0;
     // prologue: z records ZT-2 .. ZT+ZA-1 (position 0's step-0 inputs and the
     // z reads of steps the loader's progress does not cover), checked now
-    if (zin) {
+    if (zin || LIT) {  // (LIT tile 0: the z = 0 faces of those records)
       for (int rz = ZT - 2; rz < ZT + ZA; ++rz) {
         Fetch f;
-        fetch_z(rz, f);
-        if (rz < T_left && !z_ok(rz, f)) settle_z(rz, f);
+        f.z[0] = f.z[1] = 0;
+        if (zin) {
+          fetch_z(rz, f);
+          if (rz < T_left && !z_ok(rz, f)) settle_z(rz, f);
+        }
         put_z(rz, f);
       }
     }
@@ -603,11 +749,15 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       uint8_t *dst = xr0 + (s & (K0 - 1)) * SLOT + lane * REC_BYTES;
       const bool yreal = s + YOFF < T_above;
 #pragma unroll
-      for (int i = 0; i < M; ++i)
-        lds_write16(dst + i * PAIR,
-                    yreal ? make_uint4((uint32_t)f.y[2 * i], (uint32_t)(f.y[2 * i] >> 32),
-                                       (uint32_t)f.y[2 * i + 1], (uint32_t)(f.y[2 * i + 1] >> 32))
-                          : make_uint4(0u, 0u, 0u, 0u));
+      for (int i = 0; i < M; ++i) {
+        uint4 v = yreal ? make_uint4((uint32_t)f.y[2 * i], (uint32_t)(f.y[2 * i] >> 32),
+                                     (uint32_t)f.y[2 * i + 1], (uint32_t)(f.y[2 * i + 1] >> 32))
+                        : make_uint4(0u, 0u, 0u, 0u);
+        if constexpr (LIT) {
+          if (!yin) v = yface_lit(s, i);
+        }
+        lds_write16(dst + i * PAIR, v);
+      }
       put_z(rz, f);
       lds_publish(pw + 64 * NW, s + 1, lane);  // wave 0 may run step s
       fetch(s + LPD, f);
@@ -650,6 +800,25 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
         pIy[i] = pIxy[i] = pIyz[i] = pBest[i] = 0;
       }
     }
+    // LIT: the successors' symbols b_{y+1} (per half) and c_{z+1} (per position),
+    // the per-position pair score of (y+1, z+1) less GE and the [b=c] part of
+    // s3; the launch passes f_single = f_pair = 0, so the x' = 0 face column's
+    // forced inputs and the initial states are zeros
+    uint32_t bn = 0, cnl[M], UYZ[M], K1[M], lones = 0x00010001u;
+    LitArgs cv = lit;
+    if constexpr (LIT) {
+      asm volatile("" : "+v"(lones), "+v"(cv.dmS), "+v"(cv.mmE), "+v"(cv.neS));
+      bn = (y0 + 1 < lb ? SYM0 << tsa_sym(seqs, o1 + y0 + 1, pa.packed) : 0u) |
+           ((y0 + 2 < lb ? SYM0 << tsa_sym(seqs, o1 + y0 + 2, pa.packed) : 0u) << 16);
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        const int32_t z1 = q * ZT + M * lane + i + 1;
+        cnl[i] = (z1 < lc ? SYM0 << tsa_sym(seqs, o2 + z1, pa.packed) : 0u) * 0x00010001u;
+        const uint32_t ebc = pk_eq1(bn, cnl[i], lones);
+        UYZ[i] = pk_mad(ebc, cv.dmS, cv.mmE);
+        K1[i] = SOP ? pk_mad(ebc, cv.dmS, lit.mm3S) : pk_mad(ebc, lit.d1S, lit.d0S);
+      }
+    }
     // CHK: halves of real cells (row y < lb, position z < LC of the tile); the
     // rest is masked to 0, a value the monitor's range contains anyway (faces)
     uint32_t vmask[M], vmax[M], vmin[M];
@@ -665,7 +834,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
     const PencilArgs pv = F16 ? pa : pin_score_consts(pa);
     const uint32_t sel0 = lane == 0 ? 0x03020100u : 0x07060504u;  // lane 0: whole word from the face
     __syncthreads();  // the loader's prologue z records are in LDS
-    if (zin) {  // position 0 before step 0 (tools/lap_emu.py: the same initial shifts)
+    if (zin || LIT) {  // position 0 before step 0 (tools/lap_emu.py: the same initial shifts)
       const uint8_t *r1 = zring + ((ZT - 1) & (LAP_ZL - 1)) * ZREC + w * LAP_ZREC_WAVE;
       const uint8_t *r2 = zring + ((ZT - 2) & (LAP_ZL - 1)) * ZREC + w * LAP_ZREC_WAVE;
       const uint4 a0 = lds_read16(r1), a1 = lds_read16(r1 + 16);
@@ -685,11 +854,12 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       clk0 = __builtin_amdgcn_s_memtime();  // shader clock: the loop's cycles (slot 6)
     }
     // wave 0's y input: xr0 slot t % K0, or the face record (stride 0)
-    const uint8_t *const ysrc = (yin ? xr0 : yface) + lane * REC_BYTES;
-    const int32_t ystride = yin ? SLOT : 0;
+    // (LIT: always the loader's, which writes the step-varying faces)
+    const uint8_t *const ysrc = ((yin || LIT) ? xr0 : yface) + lane * REC_BYTES;
+    const int32_t ystride = (yin || LIT) ? SLOT : 0;
     // position 0's z input: zring slot (t + ZT) % ZL, or the face record
-    const uint8_t *const zsrc = (zin ? zring : zface) + w * LAP_ZREC_WAVE;
-    const int32_t zstride = zin ? ZREC : 0;
+    const uint8_t *const zsrc = ((zin || LIT) ? zring : zface) + w * LAP_ZREC_WAVE;
+    const int32_t zstride = (zin || LIT) ? ZREC : 0;
     uint32_t a_nx[M];
     load_a<M>(a_lane, a_nx);
     // producer side: my consumers' progress (y: the lap below, via the last
@@ -744,7 +914,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
 #endif
       const int32_t need = ROLE == 0 ? t + 1 : t;
       const int32_t *const pword = ROLE == 0 ? pw + 64 * NW : pw + 64 * (w - 1);
-      const bool waits = ROLE != 0 || yin || zin;
+      const bool waits = ROLE != 0 || yin || zin || LIT;
       const bool poll = waits && seen_in < need;
       int32_t fl_v = 0;
       if (poll)
@@ -787,6 +957,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       // SALU lane masks (zero outside the tile) and one bfi mask per register.
       const uint64_t lm_lo = lane_bit(klo >> LM);
       const int32_t ilo = klo & (M - 1);
+      uint32_t mx[M];  // LIT: the x' = 0 halves, whose Y is forced to 0 as it lands
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         const uint64_t ml = (M == 1 || ilo == i) ? lm_lo : 0ull;
@@ -798,22 +969,37 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
         inIxy[i] = vbfi(m1, fpv, inIxy[i]);
         inIxz[i] = vbfi(m1, fpv, inIxz[i]);
         inM[i] = vbfi(m1, 0u, inM[i]);
+        if constexpr (LIT) {
+          inIz[i] = vbfi(m1, 0u, inIz[i]);
+          inIyz[i] = vbfi(m1, 0u, inIyz[i]);
+          mx[i] = m1;
+        }
       }
       lm_hi = lm_lo;
       ihi = ilo;
       ++klo;
       // ---- the cell, up to the row above
       LapPre<M> pre;
-      if constexpr (F16)
+      LitPre<M> lpre;
+      if constexpr (LIT)
+        lit_pre<M, SOP>(lit, cv, lones, a, bn, cnl, UYZ, K1, inIx, inIz, inIxy, inIyz, inIxz, inM, lpre);
+      else if constexpr (F16)
         lap_pre_f16<M, SOP>(a, bv, c, SBC, K_, DMC, Q, pa, inIx, inIz, inIxy, inIyz, inIxz, inM, pre);
       else
         lap_pre_i16<M, SOP>(a, bv, c, Q, pv, inIx, inIz, inIxy, inIyz, inIxz, inM, pre);
       // pin the pre-cell here: left alone the compiler sinks it below the
       // progress check, so the record read's latency would not be covered
 #pragma unroll
-      for (int i = 0; i < M; ++i)
-        asm volatile("" : "+v"(pre.W[i]), "+v"(pre.N1[i]), "+v"(pre.N2[i]), "+v"(pre.N3[i]),
-                     "+v"(pre.N4[i]), "+v"(pre.N5[i]), "+v"(pre.N6[i]));
+      for (int i = 0; i < M; ++i) {
+        if constexpr (LIT) {
+          asm volatile("" : "+v"(lpre.pIx[i]), "+v"(lpre.pIy[i]), "+v"(lpre.pIz[i]), "+v"(lpre.pIxy[i]),
+                       "+v"(lpre.pIyz[i]), "+v"(lpre.pIxz[i]), "+v"(lpre.pM[i]));
+          asm volatile("" : "+v"(lpre.uxy[i]), "+v"(lpre.vxz[i]), "+v"(lpre.s3[i]));
+        } else {
+          asm volatile("" : "+v"(pre.W[i]), "+v"(pre.N1[i]), "+v"(pre.N2[i]), "+v"(pre.N3[i]),
+                       "+v"(pre.N4[i]), "+v"(pre.N5[i]), "+v"(pre.N6[i]));
+        }
+      }
 #if defined(TSA_DIAG)
       const uint64_t pt1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -848,8 +1034,15 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       const uint64_t pt2 = __builtin_amdgcn_s_memtime();
 #endif
       uint32_t oIy[M], oIxy[M], oIyz[M], oBest[M], oIz[M], oIxz[M], nIx[M];
-      if constexpr (F16) lap_post_f16<M>(pa, Ry, pre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
-      else lap_post_i16<M>(pv, Ry, pre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
+      if constexpr (LIT) {  // (oBest: the push into M, the record's fourth word)
+#pragma unroll
+        for (int i = 0; i < M; ++i) Ry[i] = vbfi(mx[i], 0u, Ry[i]);
+        lit_post<M>(lit, Ry, UYZ, lpre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
+      } else if constexpr (F16) {
+        lap_post_f16<M>(pa, Ry, pre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
+      } else {
+        lap_post_i16<M>(pv, Ry, pre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
+      }
       if constexpr (CHK) {
 #pragma unroll
         for (int i = 0; i < M; ++i) {
@@ -863,7 +1056,19 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
       if constexpr (FIN) {  // the final cell (src/TriAlign_1cyc.v:141-142,342-345)
         if (final_wg && w == (r_f >> 1)) {  // row r_f: half r_f & 1 of wave r_f / 2
 #pragma unroll
-          for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
+          for (int i = 0; i < M; ++i) {
+            if constexpr (LIT) {  // the cell's 7 inputs {M, Ix, Iy, Iz, Ixy, Iyz, Ixz}
+              fin[(0 * M + i) * 64 + lane] = inM[i];
+              fin[(1 * M + i) * 64 + lane] = inIx[i];
+              fin[(2 * M + i) * 64 + lane] = Ry[i];
+              fin[(3 * M + i) * 64 + lane] = inIz[i];
+              fin[(4 * M + i) * 64 + lane] = inIxy[i];
+              fin[(5 * M + i) * 64 + lane] = inIyz[i];
+              fin[(6 * M + i) * 64 + lane] = inIxz[i];
+            } else {
+              fin[i * 64 + lane] = oBest[i];
+            }
+          }
         }
       }
       // ---- records: to the wave below (LDS), or (last wave) the y ring
@@ -1002,7 +1207,24 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M)) void lap_kernel
     trace[(int64_t)b * LAP_TRACE_SLOTS + 4] = (unsigned long long)w_stall[0];
     trace[(int64_t)b * LAP_TRACE_SLOTS + 7] = (unsigned long long)w_bp[0];
   }
-  if (final_wg && threadIdx.x == 0) {
+  if constexpr (LIT) {
+    if (final_wg) {  // block-uniform: the final cell's 7-tuple, unshifted, and its MAX7
+      const int32_t kf = k_f, hf = r_f & 1;
+      if (threadIdx.x < 7) {
+        const uint32_t v = fin[(threadIdx.x * M + kf % M) * 64 + kf / M];
+        fin[7 * M * 64 + threadIdx.x] = (uint32_t)((int32_t)(int16_t)(uint16_t)(hf ? (v >> 16) : (v & 0xFFFF)) >> lit.sh);
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, SCOPE) == epoch;
+        int32_t best = (int32_t)fin[7 * M * 64];
+        for (int k = 1; k < 7; ++k) best = max(best, (int32_t)fin[7 * M * 64 + k]);
+        scores[tri] = bad ? TSA_SCORE_INVALID : best;  // FINAL MAX7, src/TriAlign_1cyc.v:141-142
+        if (mon != nullptr)
+          for (int k = 0; k < 7; ++k) mon[7 * (int64_t)tri + k] = (int32_t)fin[7 * M * 64 + k];
+      }
+    }
+  } else if (final_wg && threadIdx.x == 0) {
     const int32_t kf = k_f, hf = r_f & 1;
     const uint32_t v = fin[(kf % M) * 64 + kf / M];
     const uint16_t hb = (uint16_t)(hf ? (v >> 16) : (v & 0xFFFF));
@@ -1052,10 +1274,10 @@ static DevInfo dev_info() {
 // occupancy API counts waves per CU instead and reads one workgroup high at
 // the SGPR edge (MI355X_MICROARCH.md:463) and, measured, at 96 VGPRs with
 // 9-wave workgroups (it said 2, the CU ran 1).
-int lap_simd_blocks_per_cu(int M, int NW, bool f16, bool sop) {
-  char prefix[64];
-  snprintf(prefix, sizeof prefix, "_ZN3tsa10lap_kernelILi%dELi%dELb%dELb%dELb0E", M, NW, f16 ? 1 : 0,
-           sop ? 1 : 0);
+int lap_simd_blocks_per_cu(int M, int NW, bool f16, bool sop, bool lit) {
+  char prefix[80];  // lap_kernel<M, NW, F16, SOP, CHK = 0, SYS = 0, LIT>
+  snprintf(prefix, sizeof prefix, "_ZN3tsa10lap_kernelILi%dELi%dELb%dELb%dELb0ELb0ELb%dE", M, NW, f16 ? 1 : 0,
+           sop ? 1 : 0, lit ? 1 : 0);
   const int sgpr = kernel_sgpr_max(prefix), vgpr = kernel_vgpr_max(prefix);
   const int waves = std::min(sgpr_waves_per_simd(sgpr < 0 ? 112 : sgpr), vgpr_waves_per_simd(vgpr < 0 ? 256 : vgpr));
   return waves / ((NW + 1 + 3) / 4);
@@ -1063,16 +1285,20 @@ int lap_simd_blocks_per_cu(int M, int NW, bool f16, bool sop) {
 // Workgroups of one instantiation a CU holds, from the HIP occupancy API on the
 // real kernel (VGPRs, LDS) capped by the SGPR bound (the API reads one block
 // high at 81-112 SGPRs); without a device, the LDS / wave-slot model.
-template <int M, int NW, bool F16, bool SOP>
+template <int M, int NW, bool F16, bool SOP, bool LIT = false>
 static int lap_blocks_per_cu_t(size_t lds) {
   int nb = 0;
   int dev = -1;
-  const int sg = lap_simd_blocks_per_cu(M, NW, F16, SOP);
+  const int sg = lap_simd_blocks_per_cu(M, NW, F16, SOP, LIT);
   if (hipGetDevice(&dev) == hipSuccess &&
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lap_kernel<M, NW, F16, SOP, false>, 64 * (NW + 1),
-                                                   lds) == hipSuccess)
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lap_kernel<M, NW, F16, SOP, false, false, LIT>,
+                                                   64 * (NW + 1), lds) == hipSuccess)
     return std::min(nb, sg);
   return (int)std::min<size_t>(std::min<size_t>(LDS_MAX / std::max<size_t>(lds, 1), 32 / (NW + 1)), sg);
+}
+template <int M, int NW, bool SOP>
+static int lap_blocks_per_cu_lit(size_t lds) {
+  return lap_blocks_per_cu_t<M, NW, false, SOP, true>(lds);
 }
 #define TSA_LAP_SHAPES(FN, M_, NW_, F16_, SOP_, ...)                                          \
   ((M_) == 1 ? ((NW_) == 4 ? TSA_ARITH(FN, 1, 4, F16_, SOP_, __VA_ARGS__)                      \
@@ -1081,19 +1307,26 @@ static int lap_blocks_per_cu_t(size_t lds) {
                              : TSA_ARITH(FN, 2, 8, F16_, SOP_, __VA_ARGS__))                   \
                : ((NW_) == 4 ? TSA_ARITH(FN, 4, 4, F16_, SOP_, __VA_ARGS__)                    \
                              : TSA_ARITH(FN, 4, 8, F16_, SOP_, __VA_ARGS__)))
+// The literal form's shapes: M = 1, 2 and NW = 4, 8, by s3 mode
+#define TSA_LIT_SOP(FN, MM, NN, SOP_, ...) ((SOP_) ? FN<MM, NN, true>(__VA_ARGS__) : FN<MM, NN, false>(__VA_ARGS__))
+#define TSA_LIT_SHAPES(FN, M_, NW_, SOP_, ...)                                                         \
+  ((M_) == 1 ? ((NW_) == 4 ? TSA_LIT_SOP(FN, 1, 4, SOP_, __VA_ARGS__) : TSA_LIT_SOP(FN, 1, 8, SOP_, __VA_ARGS__)) \
+             : ((NW_) == 4 ? TSA_LIT_SOP(FN, 2, 4, SOP_, __VA_ARGS__) : TSA_LIT_SOP(FN, 2, 8, SOP_, __VA_ARGS__)))
 
 // Step time (us) along the chain, fitted to single-cube runs on MI355X
 // (scripts/gpu_lapvar.sh, tools/lap_trace.py): 64^3..512^3 at
 // M = 1 give 0.34-0.45 (NW = 4) and 0.42-0.48 (NW = 8), growing with the
 // workgroups per CU; M = 2 / 4 carry the round-1 fits scaled the same way --
 // the chain steps include the hand-off stalls.
-static double lap_step_us(int M, int NW, int64_t wg_per_cu) {
+// LIT: the literal cell's step, ~2.2x the message form's (an estimate, to be
+// replaced by a fit).
+static double lap_step_us(int M, int NW, int64_t wg_per_cu, bool lit = false) {
   const double base = M == 1 ? (NW == 4 ? 0.36 : 0.44) : M == 2 ? 0.55 : 0.72;
-  return base * (1.0 + 0.22 * (double)(std::max<int64_t>(wg_per_cu, 1) - 1));
+  return (lit ? 2.2 : 1.0) * base * (1.0 + 0.22 * (double)(std::max<int64_t>(wg_per_cu, 1) - 1));
 }
 
 LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW,
-                 bool full_rings, bool f16, bool sop) {
+                 bool full_rings, bool f16, bool sop, bool lit) {
 #if defined(TSA_DIAG)  // A/B knob: full-length rings (no back-pressure) on every lap launch
   if (const char *e = getenv("TSA_LAP_FULL_RINGS")) full_rings = full_rings || atoi(e) != 0;
 #endif
@@ -1108,9 +1341,12 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   const int YOFF = 2 * (NW - 1) + 1;  // lap lag of a record (kernel: YOFF)
   const int32_t T = max_la + YOFF + ZT;  // >= every workgroup's step count
   auto pow2 = [](int64_t v) { int64_t p = 1; while (p < v) p <<= 1; return (int32_t)p; };
-  g.lds = lap_lds_bytes(M, NW, max_la);
+  g.lds = lap_lds_bytes(M, NW, max_la, lit);
   const int64_t wgs = (int64_t)n * g.G * g.GZ;
-  const int per_cu = (g.lds > LDS_MAX) ? 0 : TSA_LAP_SHAPES(lap_blocks_per_cu_t, M, NW, f16, sop, g.lds);
+  if (lit && (f16 || M > 2)) return g;  // the literal form's instantiations (.ok = false)
+  const int per_cu = (g.lds > LDS_MAX) ? 0
+                     : lit             ? TSA_LIT_SHAPES(lap_blocks_per_cu_lit, M, NW, sop, g.lds)
+                                       : TSA_LAP_SHAPES(lap_blocks_per_cu_t, M, NW, f16, sop, g.lds);
   const int cus = dev_info().cus;
   // Slim rings: the lag between co-resident neighbours stays small (ring-lag
   // census, TSA_DIAG, profiles/r3e_lap_lag.jsonl): y <= 55 steps, z <= 207
@@ -1170,7 +1406,7 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   const int64_t wg_cu = std::max<int64_t>(1, std::min<int64_t>(per_cu, (wg_per_xcd + xcd_cus - 1) / xcd_cus));
   const double steps = (double)(g.G - 1) * (YOFF + LPD + 3) + (double)(g.GZ - 1) * (ZT + LPD + 2) +
                        (double)(max_la + YOFF + ZT);
-  const double chain = steps * lap_step_us(M, NW, wg_cu);
+  const double chain = steps * lap_step_us(M, NW, wg_cu, lit);
   // a later round starts as the earlier one's workgroups finish: 1024^3 (M = 2,
   // two rounds of one workgroup per CU) runs 3.04 ms against a 2.25 ms chain
   g.est_us = chain * (1.0 + 0.35 * (double)(std::max<int64_t>(g.waves, 1) - 1));
@@ -1199,12 +1435,12 @@ static uint32_t lap_next_epoch() {
   return e;
 }
 
-template <int M, int NW, bool F16, bool SOP>
-static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
-                      const LapGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
-                      hipStream_t stream, const CheckLimits *chk) {
-  if (chk && F16) return TSA_EINVAL;
-  auto kfn = chk ? lap_kernel<M, NW, F16, SOP, !F16> : lap_kernel<M, NW, F16, SOP, false>;
+typedef decltype(&lap_kernel<1, 4, true, false, false>) LapKernelFn;  // every instantiation's type
+// aux: the checked kernel's monitor words (chk), or the LIT kernel's final
+// 7-tuples (may be null)
+static int launch_lap_fn(LapKernelFn kfn, int NW, const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
+                         const LapGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
+                         const LitArgs &lit, int32_t *aux, hipStream_t stream, const CheckLimits *chk) {
   if (g.lds > LDS_MAX) return TSA_EINVAL;
   if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)g.lds) != hipSuccess)
@@ -1212,7 +1448,7 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
   int32_t *prog = (int32_t *)d_ws;
   const int64_t wgs = (int64_t)n * g.G * g.GZ;
   uint32_t *err = (uint32_t *)(prog + wgs * LAP_PROG_STRIDE);
-  int32_t *mon = prog + wgs * LAP_PROG_STRIDE + 64;  // [max(best)] n, [min(best)] n
+  int32_t *mon = chk ? prog + wgs * LAP_PROG_STRIDE + 64 : aux;  // [max(best)] n, [min(best)] n
   if (chk && (hipMemsetAsync(mon, 0x80, (size_t)n * 4, stream) != hipSuccess ||
               hipMemsetAsync(mon + n, 0x7F, (size_t)n * 4, stream) != hipSuccess))
     return TSA_EDEVICE;
@@ -1228,7 +1464,7 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
   hipLaunchKernelGGL(kfn, dim3((uint32_t)g.blocks), dim3(64 * (NW + 1)), g.lds, stream, d_seqs,
                      d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, lap_rounds(g, d_ws), prog, err,
                      d_scores, mon, pa,
-                     epoch, lap_spin_limit(), 0, g.G, yf, prog, trace);
+                     epoch, lap_spin_limit(), 0, g.G, yf, prog, trace, lit);
   if (chk) {
     if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
     hipLaunchKernelGGL(lap_certify, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, mon, n,
@@ -1261,6 +1497,36 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
     }
   }
   return TSA_OK;
+}
+template <int M, int NW, bool F16, bool SOP>
+static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
+                      const LapGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
+                      hipStream_t stream, const CheckLimits *chk) {
+  if (chk && F16) return TSA_EINVAL;
+  auto kfn = chk ? lap_kernel<M, NW, F16, SOP, !F16> : lap_kernel<M, NW, F16, SOP, false>;
+  return launch_lap_fn(kfn, NW, d_seqs, d_offsets, n, g, d_scores, d_ws, pa, LitArgs{}, nullptr, stream, chk);
+}
+template <int M, int NW, bool SOP>
+static int launch_lap_lit(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, const LapGeom &g,
+                          int32_t *d_scores, int32_t *d_final7, void *d_ws, const PencilArgs &pa,
+                          const LitArgs &lit, hipStream_t stream) {
+  return launch_lap_fn(lap_kernel<M, NW, false, SOP, false, false, true>, NW, d_seqs, d_offsets, n, g, d_scores,
+                       d_ws, pa, lit, d_final7, stream, nullptr);
+}
+
+int lap_launch_lit(const LapGeom &g, bool sop, const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
+                   int32_t *d_scores, int32_t *d_final7, void *d_ws, const KParams &kp, hipStream_t stream,
+                   int32_t **d_err) {
+  if (g.M > 2 || (g.NW != 4 && g.NW != 8)) return TSA_EINVAL;
+  if (d_err) {  // synchronous caller: clear the error word, it reads it back
+    *d_err = (int32_t *)d_ws + (int64_t)n * g.G * g.GZ * LAP_PROG_STRIDE;
+    if (hipMemsetAsync(*d_err, 0, sizeof(int32_t), stream) != hipSuccess) return TSA_EDEVICE;
+  }
+  PencilArgs pa{};  // the literal form reads only the packed flag; zero faces
+  pa.packed = kp.packed;
+  const LitArgs lit = lit_args(kp);
+  return TSA_LIT_SHAPES(launch_lap_lit, g.M, g.NW, sop, d_seqs, d_offsets, n, g, d_scores, d_final7, d_ws, pa,
+                        lit, stream);
 }
 
 int lap_launch(const LapGeom &g, bool f16, bool sop, const uint8_t *d_seqs,
@@ -1303,7 +1569,7 @@ static int launch_lap_split(const LapGeom &g, const PencilArgs &pa, const LapPar
                        q.d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, lap_rounds(g, q.d_ws), prog,
                        d_err, d_score,
                        (int32_t *)nullptr, pa, epoch, spin, q.L0, q.L1, yf_out, prog_in,
-                       (unsigned long long *)nullptr);
+                       (unsigned long long *)nullptr, LitArgs{});
     if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
   }
   return TSA_OK;

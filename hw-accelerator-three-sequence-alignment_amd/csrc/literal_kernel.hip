@@ -27,20 +27,9 @@
 // each pair target and M, 6 for the successor indicators.
 
 #include "pencil_common.h"
+#include "lap_kernel.h"
 
 namespace tsa {
-
-// Scaled constants (value << sh as int16, both halves).
-struct LitArgs {
-  uint32_t n2E, nOE, n2O;   // -2GE, -(GO+GE), -2GO
-  uint32_t dmS, mmE, nDOE;  // match - mismatch, mismatch - GE, -(GO - GE)
-  uint32_t d1S, d0S, neS;   // RTL s3 = ne + [a=b](d0 + [b=c] d1)
-  uint32_t mm3S;            // SOP s3 = 3 mismatch + dm ([a=b] + [b=c] + [a=c])
-  // pushes of a zero cell (the faces): to Ix / Iy / Iz, to a pair target with
-  // its pair score a match (1) or not (0), to M by the successor's indicators
-  uint32_t fS[3], fP[2], fM[8];
-  int32_t sh, packed;
-};
 
 constexpr int LIT_NW = 8, LIT_S = 2, LIT_RING_EXTRA = 8;
 // ring rows wave 0 prefetches (LDS-DMA): 8, 4 at M = 4 (LDS)
@@ -67,26 +56,61 @@ bool literal_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc) {
   if (max_la < 1 || max_lb < 1 || max_lc < 1 || max_lc > 512 || max_la > 4095 || max_lb > 4096) return false;
   return lit_geom(max_la, max_lb, max_lc).lds <= LDS_MAX;
 }
-bool literal_helix_chosen(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
-  if (!literal_shape_ok(max_la, max_lb, max_lc)) return false;
-  if (const char *e = getenv("TSA_PENCIL_MODE")) {
-    if (!strcmp(e, "plane")) return false;
-    if (!strcmp(e, "literal")) return true;
-  }
-  // Cost model fitted on MI355X (profiles/r3d_literal_vs_plane.jsonl): the
-  // literal helix runs T steps of 0.56 us (M = 1) / 0.95 us (M = 2) per
-  // workgroup, ~1.8x slower per step with two workgroups on every CU; PLANE
-  // runs LA+LB+LC plane launches of 4.4 us + 0.41 us per triple per 256^2
-  // (y,z) cells. A few large cubes sweep faster as planes over the chip.
+// Cost model fitted on MI355X (profiles/r3d_literal_vs_plane.jsonl): the
+// literal helix runs T steps of 0.56 us (M = 1) / 0.95 us (M = 2) per
+// workgroup, ~1.8x slower per step with two workgroups on every CU; PLANE
+// runs LA+LB+LC plane launches of 4.4 us + 0.41 us per triple per 256^2
+// (y,z) cells. A few large cubes sweep faster as planes over the chip.
+static double literal_helix_us(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
   const LitGeom g = lit_geom(max_la, max_lb, max_lc);
   const double T = (double)((max_lb + LIT_NW - 1) / LIT_NW) * g.P + LIT_S * (LIT_NW - 1) + max_lc;
   // M = 4 (208 VGPRs) runs one workgroup per CU: ~2x the M = 2 step (an estimate)
   const double waves = g.M == 4 ? (double)((n + 255) / 256)
                                 : n > 256 ? 1.8 * (double)((n + 511) / 512) : 1.0;
-  const double lit_us = T * (g.M == 1 ? 0.56 : g.M == 2 ? 0.95 : 1.9) * waves;
-  const double plane_us = (double)(max_la + max_lb + max_lc) *
-                          (4.4 + 0.41 * (double)n * (double)max_lb * (double)max_lc / 65536.0);
-  return lit_us <= plane_us;
+  return T * (g.M == 1 ? 0.56 : g.M == 2 ? 0.95 : 1.9) * waves;
+}
+static double plane_us(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  return (double)(max_la + max_lb + max_lc) *
+         (4.4 + 0.41 * (double)n * (double)max_lb * (double)max_lc / 65536.0);
+}
+// The literal lap schedule (lap_kernel LIT) for a few cubes: the geometry of
+// least estimated latency, as lap_choice picks the factored form's.
+static LapGeom literal_lap_choice(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, bool sop,
+                                  int lap) {
+  LapGeom best{};
+  best.ok = false;
+  // lap steps are counted in 13 bits (the progress words): T < 8192
+  if (lap == LAP_OFF || max_la > 4096 || max_la + 2 * 8 + 64 * 2 + 1 >= 8192) return best;
+  int m_lo = 1, m_hi = 2, nw_lo = 4, nw_hi = 8;
+  if (const char *e = getenv("TSA_LAP_M")) m_lo = m_hi = std::max(1, std::min(2, atoi(e)));  // knobs
+  if (const char *e = getenv("TSA_LAP_NW")) nw_lo = nw_hi = atoi(e) == 4 ? 4 : 8;
+  for (int M = m_lo; M <= m_hi; M *= 2)
+    for (int NW = nw_lo; NW <= nw_hi; NW *= 2) {
+      const LapGeom g = lap_geom(n, max_la, max_lb, max_lc, M, NW, false, false, sop, true);
+      if (!g.ok || g.waves > LAP_MAX_WAVES || (g.waves > 1 && g.per_cu > 1)) continue;  // as lap_choice
+      if (!best.ok || g.est_us < best.est_us) best = g;
+    }
+  return best;
+}
+int literal_kind(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, bool sop, int lap) {
+  const bool helix_ok = literal_shape_ok(max_la, max_lb, max_lc);
+  if (const char *e = getenv("TSA_PENCIL_MODE")) {  // test knobs
+    if (!strcmp(e, "plane")) return LIT_PLANE;
+    if (!strcmp(e, "literal")) return helix_ok ? LIT_HELIX : LIT_PLANE;
+    if (!strcmp(e, "litlap") && literal_lap_choice(n, max_la, max_lb, max_lc, sop, lap).ok) return LIT_LAP;
+  }
+  int kind = LIT_PLANE;
+  double best = plane_us(n, max_la, max_lb, max_lc);
+  if (helix_ok) {
+    const double h = literal_helix_us(n, max_la, max_lb, max_lc);
+    if (h <= best) { best = h; kind = LIT_HELIX; }
+  }
+  const LapGeom g = literal_lap_choice(n, max_la, max_lb, max_lc, sop, lap);
+  if (g.ok && g.est_us < best) kind = LIT_LAP;
+  return kind;
+}
+bool literal_helix_chosen(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  return literal_kind(n, max_la, max_lb, max_lc, false, LAP_OFF) == LIT_HELIX;
 }
 size_t literal_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
   return (size_t)std::min<int32_t>(n, 65535) * (size_t)lit_geom(max_la, max_lb, max_lc).ring_bytes_per_triple;
@@ -453,7 +477,7 @@ static inline int32_t wrap_bits(int64_t v, int bits) {
   const uint64_t u = (uint64_t)v << (64 - bits);
   return (int32_t)((int64_t)u >> (64 - bits));
 }
-static LitArgs lit_args(const KParams &kp) {
+LitArgs lit_args(const KParams &kp) {
   LitArgs c;
   memset(&c, 0, sizeof(c));
   const int bits = kp.bits ? kp.bits : 16;
@@ -526,6 +550,48 @@ int literal_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_
                : launch_lit<4, false>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_final7, d_ws, ca, stream);
   return sop ? launch_lit<2, true>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_final7, d_ws, ca, stream)
              : launch_lit<2, false>(d_seqs, d_offsets, n, max_lb, g, d_scores, d_final7, d_ws, ca, stream);
+}
+
+// ---------------------------------------------------------------------------
+// TSA_KERNEL_PLANE's plan: the literal lap, the literal helix or the PLANE sweep
+// (literal_kind), its workspace and its launch.
+size_t literal_plan_workspace(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, bool sop, int lap) {
+  n = std::min<int32_t>(n, 65535);
+  switch (literal_kind(n, max_la, max_lb, max_lc, sop, lap)) {
+    case LIT_LAP: return lap_workspace_bytes(literal_lap_choice(n, max_la, max_lb, max_lc, sop, lap));
+    case LIT_HELIX: return literal_workspace_bytes(n, max_la, max_lb, max_lc);
+    default: return plane_workspace_bytes(n, max_la, max_lb, max_lc);
+  }
+}
+int literal_plan_launch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, int32_t max_la, int32_t max_lb,
+                        int32_t max_lc, const KParams &kp, int32_t *d_scores, int32_t *d_final7, void *d_ws,
+                        size_t ws_bytes, hipStream_t stream, int lap, int32_t **d_err, int32_t choice_n) {
+  if (d_err) *d_err = nullptr;
+  const bool sop = kp.s3_mode == TSA_S3_SOP;
+  const int32_t cn = std::min<int32_t>(choice_n < 0 ? n : choice_n, 65535);
+  const int kind = literal_kind(cn, max_la, max_lb, max_lc, sop, lap);
+  if (kind == LIT_LAP) {
+    const LapGeom g = literal_lap_choice(cn, max_la, max_lb, max_lc, sop, lap);
+    if (n > cn || ws_bytes < lap_workspace_bytes(g)) return TSA_ENOMEM;
+    return lap_launch_lit(g, sop, d_seqs, d_offsets, n, d_scores, d_final7, d_ws, kp, stream, d_err);
+  }
+  if (kind == LIT_HELIX)
+    return literal_launch_batch(d_seqs, d_offsets, n, max_la, max_lb, max_lc, kp, d_scores, d_final7, d_ws,
+                                ws_bytes, stream);
+  return plane_launch_batch(d_seqs, d_offsets, n, max_la, max_lb, max_lc, kp, d_scores, d_final7, d_ws, ws_bytes,
+                            stream);
+}
+void literal_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, bool sop, int lap, char *buf,
+                      size_t len) {
+  n = std::min<int32_t>(n, 65535);
+  const int kind = literal_kind(n, max_la, max_lb, max_lc, sop, lap);
+  if (kind == LIT_LAP) {
+    const LapGeom g = literal_lap_choice(n, max_la, max_lb, max_lc, sop, lap);
+    snprintf(buf, len, "plane literal-lap M=%d NW=%d laps=%d tiles=%d waves=%lld", g.M, g.NW, g.G, g.GZ,
+             (long long)g.waves);
+  } else {
+    snprintf(buf, len, kind == LIT_HELIX ? "plane literal-helix" : "plane");
+  }
 }
 
 }  // namespace tsa

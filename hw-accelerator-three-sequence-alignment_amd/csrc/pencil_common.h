@@ -76,6 +76,21 @@ struct PencilArgs {
 };
 
 
+// Literal RTL arithmetic (literal_kernel.hip, the lap kernel's LIT form):
+// constants as int16 values shifted left by sh = 16 - SCORE_BITS, both halves,
+// so packed u16 adds wrap exactly at the RTL word.
+struct LitArgs {
+  uint32_t n2E, nOE, n2O;   // -2GE, -(GO+GE), -2GO
+  uint32_t dmS, mmE, nDOE;  // match - mismatch, mismatch - GE, -(GO - GE)
+  uint32_t d1S, d0S, neS;   // RTL s3 = ne + [a=b](d0 + [b=c] d1)
+  uint32_t mm3S;            // SOP s3 = 3 mismatch + dm ([a=b] + [b=c] + [a=c])
+  // pushes of a zero cell (the faces): to Ix / Iy / Iz, to a pair target with
+  // its pair score a match (1) or not (0), to M by the successor's indicators
+  uint32_t fS[3], fP[2], fM[8];
+  int32_t sh, packed;
+};
+LitArgs lit_args(const KParams &kp);
+
 // positions per lane: M packed pairs cover LC <= 128*M (1, 2, 4 or 8)
 static inline int32_t pencil_pairs(int32_t max_lc) {
   return max_lc <= 128 ? 1 : max_lc <= 256 ? 2 : max_lc <= 512 ? 4 : 8;

@@ -260,8 +260,7 @@ static int upgrade_checked(int kind, int32_t kernel, int32_t n, const tsa_params
 static size_t workspace_for(int kind, int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
                             const tsa_params *p, LapPolicy lap = LAP_RESIDENT) {
   if (kind == TSA_KERNEL_PLANE)
-    return literal_helix_chosen(n, max_la, max_lb, max_lc) ? literal_workspace_bytes(n, max_la, max_lb, max_lc)
-                                                           : plane_workspace_bytes(n, max_la, max_lb, max_lc);
+    return literal_plan_workspace(n, max_la, max_lb, max_lc, p->s3_mode == TSA_S3_SOP, lap);
   KParams kp;
   if (build_kparams(p, &kp)) return 0;
   return pencil_workspace_bytes(n, max_la, max_lb, max_lc, kp, value_bound(p, max_la, max_lb, max_lc),
@@ -286,11 +285,8 @@ static int launch_kind(int kind, const uint8_t *d_seqs, const int64_t *d_off, in
   if (rc) return rc;
   kp.packed = packed;
   if (kind == TSA_KERNEL_PLANE)
-    return literal_helix_chosen(choice_n < 0 ? n : choice_n, max_la, max_lb, max_lc)
-               ? literal_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp, d_scores, d_final7, ws,
-                                      ws_bytes, s)
-               : plane_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp, d_scores, d_final7,
-                                    ws, ws_bytes, s);
+    return literal_plan_launch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp, d_scores, d_final7, ws, ws_bytes, s,
+                               lap, d_err, choice_n);
   const CheckLimits lim = check_limits(p);
   return pencil_launch_batch(d_seqs, d_off, n, max_la, max_lb, max_lc, kp,
                              value_bound(p, max_la, max_lb, max_lc), d_scores, ws, ws_bytes, s,
@@ -321,12 +317,15 @@ static int run_host_batch_on_device(int device, const uint8_t *seqs, const int64
   if (!final7) kind = upgrade_checked(kind, kernel, n, p, max_la, max_lb, max_lc);
   // chunk so the workspace stays under ~8 GiB and the grid under 65535
   // triples; the workspace is what the chunk's own plan (lap for a few cubes,
-  // the helix ring otherwise) and its fallback (helix; PLANE for the checked
-  // kernel) need
+  // the helix ring otherwise) and its fallbacks (the same kind without the lap
+  // schedule; the literal kinds for the checked kernel) need
   auto ws_of = [&](int32_t c) {
-    return std::max(workspace_for(kind, c, max_la, max_lb, max_lc, p, LAP_STREAM),
-                    kind == TSA_KERNEL_CHECKED ? workspace_for(TSA_KERNEL_PLANE, c, max_la, max_lb, max_lc, p)
-                                               : workspace_for(kind, c, max_la, max_lb, max_lc, p, LAP_OFF));
+    size_t w = std::max(workspace_for(kind, c, max_la, max_lb, max_lc, p, LAP_STREAM),
+                        workspace_for(kind, c, max_la, max_lb, max_lc, p, LAP_OFF));
+    if (kind == TSA_KERNEL_CHECKED)
+      w = std::max({w, workspace_for(TSA_KERNEL_PLANE, c, max_la, max_lb, max_lc, p, LAP_STREAM),
+                    workspace_for(TSA_KERNEL_PLANE, c, max_la, max_lb, max_lc, p, LAP_OFF)});
+    return w;
   };
   const size_t cap = (size_t)8 << 30;
   int32_t chunk = std::min(n, 65535);
@@ -356,6 +355,23 @@ static int run_host_batch_on_device(int device, const uint8_t *seqs, const int64
   HIPCHK(hipMemcpyAsync(d_off, off.data(), off.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(d_ws, 0, ws_bytes, s));
   for (int32_t c0 = 0; c0 < n && rc == TSA_OK; c0 += chunk) {
+    // a lap launch whose hand-off timed out (*d_err set) is rescored by the
+    // same kind without the lap schedule (no cross-workgroup dependency)
+    auto lap_rescue = [&](int k, int32_t cn, int32_t *d_err, int32_t *fin) -> int {
+      int32_t herr = 0;
+      if (hipMemcpyAsync(&herr, d_err, sizeof(herr), hipMemcpyDeviceToHost, s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess)
+        return TSA_EDEVICE;
+      if (!herr) return TSA_OK;
+      g_lap_fallbacks.fetch_add(1);
+      fprintf(stderr, "trialign: lap hand-off timed out on device %d (%d triples); rescoring "
+                      "without the lap schedule\n", device, cn);
+      int32_t *d_err2 = nullptr;
+      int r = launch_kind(k, d_seqs, d_off + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p, d_scores + c0, fin,
+                          d_ws, ws_bytes, s, LAP_OFF, &d_err2);
+      if (r == TSA_OK && d_err2) r = TSA_EINTERNAL;  // LAP_OFF never plans a lap grid
+      return r;
+    };
     const int32_t cn = std::min(chunk, n - c0);
     int32_t *d_err = nullptr;
     rc = launch_kind(kind, d_seqs, d_off + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p,
@@ -374,24 +390,13 @@ static int run_host_batch_on_device(int device, const uint8_t *seqs, const int64
       if (herr || bad) {
         g_check_fallbacks.fetch_add(herr ? cn : bad);
         if (herr) g_lap_fallbacks.fetch_add(1);
+        int32_t *d_err3 = nullptr;  // the literal kinds (lap, helix or plane)
         rc = launch_kind(TSA_KERNEL_PLANE, d_seqs, d_off + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc,
-                         p, d_scores + c0, nullptr, d_ws, ws_bytes, s, LAP_RESIDENT, nullptr, 0, chunk);
+                         p, d_scores + c0, nullptr, d_ws, ws_bytes, s, LAP_STREAM, &d_err3, 0, chunk);
+        if (rc == TSA_OK && d_err3) rc = lap_rescue(TSA_KERNEL_PLANE, cn, d_err3, nullptr);
       }
     } else if (rc == TSA_OK && d_err) {  // lap kernel: a timed-out hand-off invalidates the chunk
-      int32_t herr = 0;
-      HIPCHK(hipMemcpyAsync(&herr, d_err, sizeof(herr), hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-      if (herr) {
-        // rescore with the helix kernel, which has no cross-workgroup
-        // dependency and cannot time out
-        g_lap_fallbacks.fetch_add(1);
-        fprintf(stderr, "trialign: lap hand-off timed out on device %d (%d triples); rescoring "
-                        "with the helix kernel\n", device, cn);
-        int32_t *d_err2 = nullptr;
-        rc = launch_kind(kind, d_seqs, d_off + 3 * (int64_t)c0, cn, max_la, max_lb, max_lc, p,
-                         d_scores + c0, nullptr, d_ws, ws_bytes, s, LAP_OFF, &d_err2);
-        if (rc == TSA_OK && d_err2) rc = TSA_EINTERNAL;  // LAP_OFF never plans a lap grid
-      }
+      rc = lap_rescue(kind, cn, d_err, d_final ? d_final + 7 * (int64_t)c0 : nullptr);
     }
   }
   if (rc) goto done;
@@ -490,6 +495,7 @@ int tsa_score_gpu_multi(const uint8_t *a, int32_t la, const uint8_t *b, int32_t 
   const int64_t off[4] = {0, la, (int64_t)la + lb, (int64_t)la + lb + lc};
   std::vector<LapPart> parts((size_t)np);
   std::vector<void *> ws((size_t)np, nullptr);
+  std::vector<char> own((size_t)np, 0);  // part i created its stream
   int32_t *d_score = nullptr;
   uint32_t *d_err = nullptr;
   int32_t h_score = 0;
@@ -518,7 +524,15 @@ int tsa_score_gpu_multi(const uint8_t *a, int32_t la, const uint8_t *b, int32_t 
     q.L0 = (int32_t)((int64_t)g.G * i / np);
     q.L1 = (int32_t)((int64_t)g.G * (i + 1) / np);
     HIPCHK(hipSetDevice(q.device));
-    HIPCHK(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
+    // parts sharing a device run one after another on the first one's stream:
+    // launched concurrently, a later part's workgroups can take the CU slots
+    // an earlier part's undispatched workgroups need, and wait on them (two
+    // 256-workgroup parts of 1024^3 at one workgroup per CU timed out). In lap
+    // order with full-length rings an earlier part never waits on a later one.
+    for (int j = 0; j < i && !q.stream; ++j)
+      if (parts[j].device == q.device) q.stream = parts[j].stream;
+    own[i] = q.stream == nullptr;
+    if (own[i]) HIPCHK(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
     uint8_t *ds = nullptr;
     int64_t *dof = nullptr;
     // fine-grained: its neighbours' stores land here and are polled here
@@ -580,7 +594,7 @@ done:
     if (parts[i].d_offsets) (void)hipFree((void *)parts[i].d_offsets);
     if (ws[i]) (void)hipFree(ws[i]);
     if (i == np - 1 && d_score) (void)hipFree(d_score);
-    if (parts[i].stream) (void)hipStreamDestroy(parts[i].stream);
+    if (parts[i].stream && own[i]) (void)hipStreamDestroy(parts[i].stream);
   }
   return rc;
 }
@@ -662,12 +676,11 @@ int tsa_describe_plan(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
   int kind = choose_kernel(kernel, p, max_la, max_lb, max_lc);
   if (kind < 0) return TSA_ERANGE;
   if (sync) kind = upgrade_checked(kind, kernel, n, p, max_la, max_lb, max_lc);
+  const LapPolicy lap = sync ? LAP_STREAM : LAP_RESIDENT;
   if (kind == TSA_KERNEL_PLANE) {
-    snprintf(buf, len, literal_helix_chosen(std::min(n, 65535), max_la, max_lb, max_lc) ? "plane literal-helix"
-                                                                                         : "plane");
+    literal_describe(n, max_la, max_lb, max_lc, p->s3_mode == TSA_S3_SOP, lap, buf, len);
     return TSA_OK;
   }
-  const LapPolicy lap = sync ? LAP_STREAM : LAP_RESIDENT;
   if (kind == TSA_KERNEL_CHECKED && !checked_plan(n, p, max_la, max_lb, max_lc, lap)) return TSA_ERANGE;
   KParams kp;
   build_kparams(p, &kp);

@@ -71,10 +71,22 @@ size_t literal_workspace_bytes(int32_t n, int32_t max_la, int32_t max_lb, int32_
 int literal_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, int32_t max_la,
                          int32_t max_lb, int32_t max_lc, const KParams &kp, int32_t *d_scores,
                          int32_t *d_final7, void *d_ws, size_t ws_bytes, hipStream_t stream);
-// Which literal kernel a batch runs: the literal helix (batches the helix
-// shape holds) or the plane sweep (single cubes, LC > 256, traceback).
-// TSA_PENCIL_MODE=plane / =literal force one (tests).
+// Which literal kernel a batch runs (TSA_KERNEL_PLANE): the literal lap
+// schedule (a few cubes, lap_kernel LIT), the literal helix (batches the
+// helix shape holds) or the plane sweep (the rest; traceback), by a cost
+// model. lap: a LapPolicy (LAP_OFF: no lap). TSA_PENCIL_MODE=plane / literal
+// / litlap force one (tests).
+enum LitKind { LIT_PLANE = 0, LIT_HELIX = 1, LIT_LAP = 2 };
+int literal_kind(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, bool sop, int lap);
 bool literal_helix_chosen(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc);
+size_t literal_plan_workspace(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, bool sop, int lap);
+// d_err (synchronous callers, lap plans only): as pencil_launch_batch's.
+// choice_n: the batch size the workspace was sized for.
+int literal_plan_launch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, int32_t max_la, int32_t max_lb,
+                        int32_t max_lc, const KParams &kp, int32_t *d_scores, int32_t *d_final7, void *d_ws,
+                        size_t ws_bytes, hipStream_t stream, int lap, int32_t **d_err, int32_t choice_n);
+void literal_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, bool sop, int lap, char *buf,
+                      size_t len);
 
 // Traceback: pointer cube of one (la,lb,lc) triple and the walk kernel.
 size_t tb_cube_bytes(int32_t la, int32_t lb, int32_t lc);

@@ -70,8 +70,15 @@ def test_validate(tsa):
 def test_workspace_size(tsa, monkeypatch):
     p = tsa.TsaParams.default()
     # the literal helix: one ring of (P + 8) records x M x 64 lanes x 16 B per triple
+    monkeypatch.setenv("TSA_PENCIL_MODE", "literal")
     lit = tsa.workspace_size(4, 64, 64, 64, p, "plane")
     assert lit == 4 * (128 + 8) * 64 * 16
+    # the literal lap (what the cost model picks for a few small cubes): O(N^2)
+    monkeypatch.delenv("TSA_PENCIL_MODE")
+    assert tsa.describe_plan(4, 64, 64, 64, p, kernel="plane").startswith("plane literal-lap")
+    ll = tsa.workspace_size(1, 256, 256, 256, p, "plane")
+    assert tsa.describe_plan(1, 512, 512, 512, p, kernel="plane").startswith("plane literal-lap")
+    assert 1.5 < tsa.workspace_size(1, 512, 512, 512, p, "plane") / ll < 6
     monkeypatch.setenv("TSA_PENCIL_MODE", "plane")  # the plane sweep itself
     n1 = tsa.workspace_size(1, 64, 64, 64, p, "plane")
     n4 = tsa.workspace_size(4, 64, 64, 64, p, "plane")
@@ -112,15 +119,24 @@ def test_describe_plan(tsa):
     assert tsa.describe_plan(1, 1024, 1024, 1024, p16).startswith("pencil lap i16 rtl")
     sop = tsa.TsaParams.default(s3_mode=tsa.S3_SOP)
     assert " sop " in tsa.describe_plan(512, 256, 256, 256, sop)
-    # the literal kernels: the literal helix where its cost model beats the
-    # plane sweep (small cubes, batches), PLANE for a few large cubes
-    assert tsa.describe_plan(4, 64, 64, 64, p, kernel="plane") == "plane literal-helix"
+    # the literal kernels by their cost model: the literal lap for a few cubes
+    # (lap_kernel LIT), the literal helix for batches, the plane sweep where
+    # neither runs (many cubes with LC > 512)
+    assert tsa.describe_plan(4, 64, 64, 64, p, kernel="plane").startswith("plane literal-lap M=1")
     assert tsa.describe_plan(512, 256, 256, 256, p, kernel="plane") == "plane literal-helix"
-    assert tsa.describe_plan(1, 256, 256, 256, p, kernel="plane") == "plane"
-    assert tsa.describe_plan(4, 512, 512, 512, p, kernel="plane") == "plane"  # LC > 256
+    assert tsa.describe_plan(1, 256, 256, 256, p, kernel="plane").startswith("plane literal-lap")
+    assert tsa.describe_plan(1, 1024, 1024, 1024, p, kernel="plane").startswith("plane literal-lap M=2 NW=8")
+    assert tsa.describe_plan(64, 1024, 1024, 1024, p, kernel="plane") == "plane"
+    # without the lap schedule (the helix / sweep rescue of a timed-out lap)
+    os.environ["TSA_PENCIL_MODE"] = "literal"
+    try:
+        assert tsa.describe_plan(4, 64, 64, 64, p, kernel="plane") == "plane literal-helix"
+    finally:
+        del os.environ["TSA_PENCIL_MODE"]
     # gap_extend > gap_open: the widened message groups are not exact -> literal
     ge = tsa.TsaParams.default(gap_open=1, gap_extend=2)
-    assert tsa.describe_plan(4, 64, 64, 64, ge) == "plane literal-helix"
+    assert tsa.describe_plan(4, 64, 64, 64, ge).startswith("plane literal-lap")
+    assert tsa.describe_plan(512, 64, 64, 64, ge) == "plane literal-helix"
     with pytest.raises(tsa.TsaError) as e:
         tsa.describe_plan(4, 64, 64, 64, ge, kernel="pencil")
     assert e.value.rc == tsa.TSA_ERANGE
@@ -128,10 +144,10 @@ def test_describe_plan(tsa):
     # the synchronous path tries the checked lap kernel first (PLANE rescoring
     # whatever it cannot certify), and so does an explicit kernel="checked"
     p6 = tsa.TsaParams.default(score_bits=6)
-    assert tsa.describe_plan(4, 90, 90, 90, p6, sync=False) == "plane literal-helix"
+    assert tsa.describe_plan(4, 90, 90, 90, p6, sync=False).startswith("plane literal-lap")
     assert tsa.describe_plan(4, 90, 90, 90, p6, sync=True).endswith(" checked")
     assert tsa.describe_plan(1, 1024, 1024, 1024, p, sync=True).startswith("pencil lap i16 rtl")
-    assert tsa.describe_plan(1, 1024, 1024, 1024, p, sync=False) == "plane"
+    assert tsa.describe_plan(1, 1024, 1024, 1024, p, sync=False).startswith("plane literal-lap M=2 NW=8")
     assert tsa.describe_plan(1, 1024, 1024, 1024, p, kernel="checked", sync=False).endswith(" checked")
     # a batch too large for the lap schedule is never checked
     assert tsa.describe_plan(4096, 800, 800, 800, p, sync=True) == "plane"

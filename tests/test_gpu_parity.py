@@ -753,3 +753,75 @@ def test_literal_helix_final_states_and_wrap(gpu, orc, golden, monkeypatch):
     ref = orc.score(a, a, a, o9, final_states=True)
     s, fin = gpu.score(a, a, a, p9, final_states=True)
     assert (s, tuple(fin)) == ref and ref[0] != 360
+
+
+# ---- the literal lap schedule (lap_kernel LIT): TSA_KERNEL_PLANE's single-cube path
+LIT_GEOMS = [("1", "4"), ("1", "8"), ("2", "4"), ("2", "8")]
+
+
+@pytest.mark.parametrize("m,nw", LIT_GEOMS)
+@pytest.mark.parametrize("bits,s3_mode", [(12, 0), (6, 1), (16, 0)])
+def test_literal_lap_matches_oracle(gpu, orc, monkeypatch, m, nw, bits, s3_mode):
+    """The RTL's literal arithmetic on the single-cube lap schedule
+    (tools/litlap_emu.py replays it): scores and final 7-tuples equal the
+    oracle's on ragged cubes over several laps and z-tiles, related and
+    homopolymer triples, narrow words that wrap, both s3 modes."""
+    monkeypatch.setenv("TSA_PENCIL_MODE", "litlap")
+    monkeypatch.setenv("TSA_LAP_M", m)
+    monkeypatch.setenv("TSA_LAP_NW", nw)
+    rng = np.random.default_rng(300 + 7 * int(m) + int(nw) + bits + s3_mode)
+    p, op = gpu.TsaParams.default(score_bits=bits, s3_mode=s3_mode), orc.default_params(score_bits=bits, s3_mode=s3_mode)
+    shapes = [(64, 64, 64), (37, 70, 131), (90, 17, 65), (5, 33, 200), (120, 9, 129)]
+    cases = [tuple(rng.integers(0, 5, n).astype(np.uint8) for n in sh) for sh in shapes]
+    h = rng.integers(0, 4, 150).astype(np.uint8)
+    cases.append((h, h[:41].copy(), h[:140].copy()))                     # related: high scores
+    z = np.zeros(100, np.uint8)
+    cases.append((z, z[:50].copy(), z[:90].copy()))                      # homopolymer (wraps at 6 bits)
+    for a, b, c in cases:
+        plan = gpu.describe_plan(1, len(a), len(b), len(c), p, kernel="plane", sync=True)
+        assert plan.startswith(f"plane literal-lap M={m} NW={nw}"), plan
+        s, fin = gpu.score(a, b, c, p, kernel="plane", final_states=True)
+        assert (s, tuple(fin)) == orc.score(a, b, c, op, final_states=True), (len(a), len(b), len(c), plan)
+
+
+def test_literal_lap_batch_and_go_below_ge(gpu, orc, monkeypatch):
+    """A batch of ragged cubes in one literal lap launch (columns of several
+    triples) through the async entry point, and a parameter set the factored
+    form cannot run (GO < GE), whose AUTO plan is then the literal lap."""
+    import torch
+    rng = np.random.default_rng(77)
+    triples = [tuple(rng.integers(0, 5, int(rng.integers(20, 160))).astype(np.uint8) for _ in range(3))
+               for _ in range(5)]
+    p, op = gpu.TsaParams.default(score_bits=9), orc.default_params(score_bits=9)
+    ml = [max(len(t[k]) for t in triples) for k in range(3)]
+    monkeypatch.setenv("TSA_PENCIL_MODE", "litlap")
+    assert gpu.describe_plan(len(triples), *ml, p, kernel="plane").startswith("plane literal-lap")
+    seqs, offs = gpu.pack_batch(triples)
+    ws = gpu.workspace_size(len(triples), *ml, p, "plane")
+    d_seqs, d_offs = torch.from_numpy(seqs).cuda(), torch.from_numpy(offs).cuda()
+    d_sc = torch.zeros(len(triples), dtype=torch.int32, device="cuda")
+    d_ws = torch.zeros(max(ws, 16), dtype=torch.uint8, device="cuda")
+    gpu.score_batch_async(d_seqs.data_ptr(), d_offs.data_ptr(), len(triples), *ml, d_sc.data_ptr(),
+                          d_ws.data_ptr(), ws, torch.cuda.current_stream().cuda_stream, p, "plane")
+    torch.cuda.synchronize()
+    assert np.array_equal(d_sc.cpu().numpy(), orc.score_batch(seqs, offs, op, nthreads=8))
+    monkeypatch.delenv("TSA_PENCIL_MODE")
+    kw = dict(gap_open=1, gap_extend=2, score_bits=12)
+    p2, o2 = gpu.TsaParams.default(**kw), orc.default_params(**kw)
+    a, b, c = (rng.integers(0, 4, 256).astype(np.uint8) for _ in range(3))
+    assert gpu.describe_plan(1, 256, 256, 256, p2, kernel="auto", sync=True).startswith("plane literal-lap")
+    assert gpu.score(a, b, c, p2) == orc.score(a, b, c, o2)
+
+
+def test_literal_lap_1024_rtl_words(gpu, orc, synth):
+    """configs[3]'s 1024^3 cube in the RTL's literal 12-bit arithmetic on the
+    literal lap (kernel=plane): the score and final 7-tuple equal the
+    oracle's, with no lap fallback."""
+    a, b, c = synth.triple(3, 1024)
+    p, op = gpu.TsaParams.default(score_bits=12), orc.default_params(score_bits=12)
+    plan = gpu.describe_plan(1, 1024, 1024, 1024, p, kernel="plane", sync=True)
+    assert plan.startswith("plane literal-lap"), plan
+    before = gpu.fallback_count()
+    s, fin = gpu.score(a, b, c, p, kernel="plane", final_states=True)
+    assert (s, tuple(fin)) == orc.score(a, b, c, op, final_states=True)
+    assert gpu.fallback_count() == before

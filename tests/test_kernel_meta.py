@@ -62,27 +62,33 @@ def sgpr_waves(sgpr):
 @pytest.mark.parametrize("M", [1, 2, 4])
 @pytest.mark.parametrize("NW", [4, 8])
 def test_lap_residency_sgpr_cap(tsa, meta, M, NW):
-    """lap_simd_blocks_per_cu(M, NW, f16, sop) = the SGPR / VGPR waves per SIMD
-    over the waves a workgroup may put on one SIMD, from the table's worst
-    variant."""
-    fn = getattr(tsa.lib(), "_ZN3tsa22lap_simd_blocks_per_cuEiibb")
+    """lap_simd_blocks_per_cu(M, NW, f16, sop, lit) = the SGPR / VGPR waves per
+    SIMD over the waves a workgroup may put on one SIMD, from the table's
+    single-device instantiation (CHK = SYS = 0) of that form; the literal form
+    (LIT, int16, M <= 2) has its own."""
+    fn = getattr(tsa.lib(), "_ZN3tsa22lap_simd_blocks_per_cuEiibbb")
     fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_bool, ctypes.c_bool]
-    for f16 in (False, True):
-        for sop in (False, True):
-            pre = f"_ZN3tsa10lap_kernelILi{M}ELi{NW}ELb{int(f16)}ELb{int(sop)}ELb0E"
-            sg = max(v["sgpr"] for k, v in meta.items() if k.startswith(pre))
-            vg = max(v["vgpr"] + v.get("agpr", 0) for k, v in meta.items() if k.startswith(pre))
-            want = min(sgpr_waves(sg), vgpr_waves(vg)) // ((NW + 1 + 3) // 4)
-            assert fn(M, NW, f16, sop) == want
-            assert want >= 1
+    fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_bool, ctypes.c_bool, ctypes.c_bool]
+    forms = [(f16, sop, False) for f16 in (False, True) for sop in (False, True)]
+    if M <= 2:
+        forms += [(False, sop, True) for sop in (False, True)]
+    for f16, sop, lit in forms:
+        pre = f"_ZN3tsa10lap_kernelILi{M}ELi{NW}ELb{int(f16)}ELb{int(sop)}ELb0ELb0ELb{int(lit)}E"
+        sg = max(v["sgpr"] for k, v in meta.items() if k.startswith(pre))
+        vg = max(v["vgpr"] + v.get("agpr", 0) for k, v in meta.items() if k.startswith(pre))
+        want = min(sgpr_waves(sg), vgpr_waves(vg)) // ((NW + 1 + 3) // 4)
+        assert fn(M, NW, f16, sop, lit) == want, (f16, sop, lit)
+        assert want >= 1
+    if M <= 2:  # the literal form keeps its registers in registers
+        lit = [k for k in meta if re.match(rf"_ZN3tsa10lap_kernelILi{M}ELi{NW}ELb0ELb[01]ELb0ELb0ELb1EE", k)]
+        assert len(lit) == 2 and all(meta[k].get("scratch", 0) == 0 for k in lit)
     # measured (tools/lap_trace.py start stamps): M = 1 NW = 8 runs two
     # 9-wave workgroups per CU; M = 2 (96 VGPRs, 5 waves per SIMD) one -- the
     # occupancy API said 2 -- so its 1024^3 grid runs two dispatch rounds
     if NW == 8 and M == 1:
-        assert fn(M, NW, False, False) == 2
+        assert fn(M, NW, False, False, False) == 2
     if NW == 8 and M == 2:
-        assert fn(M, NW, False, False) == 1
+        assert fn(M, NW, False, False, False) == 1
     # the edge the guide names: 97-112 SGPRs leave 6 waves per SIMD, 7 below it
     assert sgpr_waves(106) == 6 and sgpr_waves(80) == 8
     assert vgpr_waves(96) == 5 and vgpr_waves(80) == 6
