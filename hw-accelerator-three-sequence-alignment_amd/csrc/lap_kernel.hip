@@ -1318,11 +1318,12 @@ static int lap_blocks_per_cu_lit(size_t lds) {
 // M = 1 give 0.34-0.45 (NW = 4) and 0.42-0.48 (NW = 8), growing with the
 // workgroups per CU; M = 2 / 4 carry the round-1 fits scaled the same way --
 // the chain steps include the hand-off stalls.
-// LIT: the literal cell's step, ~2.2x the message form's (an estimate, to be
-// replaced by a fit).
+// LIT: the literal cell's step, 1.3-1.5x the message form's (single cubes
+// 64^3 .. 1024^3 on MI355X, profiles/r3l_literal_lap_vs_plane.jsonl against
+// the r3h bench's lap timings).
 static double lap_step_us(int M, int NW, int64_t wg_per_cu, bool lit = false) {
   const double base = M == 1 ? (NW == 4 ? 0.36 : 0.44) : M == 2 ? 0.55 : 0.72;
-  return (lit ? 2.2 : 1.0) * base * (1.0 + 0.22 * (double)(std::max<int64_t>(wg_per_cu, 1) - 1));
+  return (lit ? 1.45 : 1.0) * base * (1.0 + 0.22 * (double)(std::max<int64_t>(wg_per_cu, 1) - 1));
 }
 
 LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW,
