@@ -384,7 +384,8 @@ def single_specs(args, L):
     times: configs[2] (L^3, the batch's words), configs[1] (64^3), the
     paper's 128^3 and 512^3 (Table III, RTL 12-bit words) and configs[3]
     (1024^3 with 16-bit words, and with the RTL's 12-bit words on the checked
-    kernel)."""
+    kernel), and 512^3 / 1024^3 in the literal arithmetic (kernel=plane: the
+    literal lap kernel)."""
     specs = [(f"configs[2]: {L}^3", L, args.score_bits, 7, None)]
     if not args.no_extra_configs:
         specs += [("configs[1]: 64^3", 64, args.score_bits, 15, None),
@@ -392,7 +393,10 @@ def single_specs(args, L):
                   ("paper N=512: 512^3", 512, args.score_bits, 5, None),
                   ("configs[3]: 1024^3 (16-bit words)", 1024, 16, 5, None),
                   # the score is exact, or TSA_SCORE_UNCERTIFIED (then rescored by PLANE)
-                  ("configs[3]: 1024^3 (12-bit RTL words, checked)", 1024, 12, 5, "checked")]
+                  ("configs[3]: 1024^3 (12-bit RTL words, checked)", 1024, 12, 5, "checked"),
+                  # the RTL's literal wrapped arithmetic (TSA_KERNEL_PLANE: the literal lap)
+                  ("paper N=512: 512^3 (literal arithmetic)", 512, 12, 5, "plane"),
+                  ("configs[3]: 1024^3 (12-bit RTL words, literal arithmetic)", 1024, 12, 5, "plane")]
     return specs
 
 

@@ -192,13 +192,13 @@ def device_count() -> int:
 
 def fallback_count() -> int:
     """Lap hand-offs that timed out on the synchronous paths so far (each was
-    rescored by the helix kernel); 0 in a healthy run."""
+    rescored without the lap schedule); 0 in a healthy run."""
     return int(_lib.tsa_fallback_count())
 
 
 def check_fallback_count() -> int:
     """Triples the checked kernel could not certify on the synchronous paths
-    so far (each was rescored by the literal PLANE kernel)."""
+    so far (each was rescored in the literal arithmetic, kernel="plane")."""
     return int(_lib.tsa_check_fallback_count())
 
 
@@ -241,7 +241,7 @@ def score(a, b, c, params: Optional[TsaParams] = None, kernel: str | int = "auto
     """Optimal 3-D DP score of one triple on GPU ``device``.
 
     ``final_states=True`` also returns the 7 states {M,Ix,Iy,Iz,Ixy,Iyz,Ixz}
-    of cell (LA,LB,LC) (runs the plane kernel)."""
+    of cell (LA,LB,LC) (runs the literal kernels: kernel="plane")."""
     p = params or TsaParams.default()
     A, B, C = _as_u8(a), _as_u8(b), _as_u8(c)
     k = KERNELS[kernel] if isinstance(kernel, str) else int(kernel)

@@ -73,7 +73,11 @@ extern "C" {
 
 /* Kernel selection for tsa_score_*; TSA_KERNEL_AUTO picks per shape. */
 #define TSA_KERNEL_AUTO 0
-#define TSA_KERNEL_PLANE 1  /* anti-diagonal plane sweep, literal RTL arithmetic */
+/* The literal RTL arithmetic (every candidate wrapped at SCORE_BITS) for any
+ * parameter set. Its plan by a cost model: the literal lap schedule for a few
+ * cubes, the literal helix for batches of LC <= 512, else the anti-diagonal
+ * plane sweep (tsa_describe_plan names it). */
+#define TSA_KERNEL_PLANE 1
 #define TSA_KERNEL_PENCIL 2 /* register-systolic pencil sweep (factored form)    */
 /* The pencil lap kernel in int16 with a range monitor, for cubes whose a-priori
  * bound exceeds SCORE_BITS (beyond ~680 per side with the RTL constants) but
@@ -103,16 +107,15 @@ void tsa_default_params(tsa_params *p);
 int tsa_validate(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
                  const uint8_t *c, int32_t lc, const tsa_params *p);
 
-/* Score one triple on HIP device `device` (synchronous). Host buffers.
- * final_states (nullable) receives the 7 states {M,Ix,Iy,Iz,Ixy,Iyz,Ixz} of
- * cell (la,lb,lc) -- the 84-bit SRAM word of src/TriAlign_1cyc.v:130,138 --
- * and is only filled by the PLANE kernel (TSA_KERNEL_PLANE); other kernels
- * leave it untouched. */
+/* Score one triple on HIP device `device` (synchronous). Host buffers. */
 int tsa_score_gpu(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
                   const uint8_t *c, int32_t lc, const tsa_params *p,
                   int32_t *score, int32_t device);
 
-/* As tsa_score_gpu with an explicit kernel choice and optional final states. */
+/* As tsa_score_gpu with an explicit kernel choice and optional final states:
+ * final_states (nullable) receives the 7 states {M,Ix,Iy,Iz,Ixy,Iyz,Ixz} of
+ * cell (la,lb,lc) -- the 84-bit SRAM word of src/TriAlign_1cyc.v:130,138; a
+ * non-null final_states runs the literal kernels (TSA_KERNEL_PLANE). */
 int tsa_score_gpu_ex(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
                      const uint8_t *c, int32_t lc, const tsa_params *p,
                      int32_t kernel, int32_t *score, int32_t *final_states,
@@ -212,12 +215,14 @@ int tsa_describe_plan(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
                       size_t len);
 
 /* Lap-kernel hand-offs that timed out on the synchronous entry points since
- * the library was loaded; each was rescored with the helix kernel (and logged
- * to stderr). 0 in a healthy run. */
+ * the library was loaded; each was rescored without the lap schedule (the
+ * helix, or for the literal arithmetic the literal helix / plane sweep) and
+ * logged to stderr. 0 in a healthy run. */
 int64_t tsa_fallback_count(void);
 
 /* Triples the checked kernel could not certify on the synchronous entry points
- * since the library was loaded; each was rescored with the PLANE kernel. */
+ * since the library was loaded; each was rescored in the literal arithmetic
+ * (TSA_KERNEL_PLANE's plan). */
 int64_t tsa_check_fallback_count(void);
 
 /* Number of visible HIP devices (0 when none), or a negative code. */
