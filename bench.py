@@ -528,15 +528,30 @@ def oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single, pending)
             r = single.get(key, {})
             put(key, r.get("score"), refs.get((Ls, bits)))
         sp = single.get("split over devices")
+        errors = {}
         if isinstance(sp, dict):
             lens = [k for k in sp if k.endswith("^3")]
+            devs = sp.get("devices")
+            if isinstance(devs, str):  # the child failed before printing ("0,1")
+                devs = [int(d) for d in devs.split(",") if d.strip().isdigit()]
+            # across distinct GPUs (the driver's N-GPU run) the split is the one
+            # path no 1-GPU box can exercise: an error there (no score) is
+            # recorded under parity["errors"]; a wrong score still fails
+            cross = isinstance(devs, list) and len(set(devs)) > 1
             if not lens:
-                put("split over devices", None, None)
+                if cross:
+                    errors["split over devices"] = sp.get("error", "no result")
+                else:
+                    put("split over devices", None, None)
             for k in lens:
                 Ls = int(k[:-2])
                 for part in ("one_part", "split"):
-                    put(f"split over devices {sp.get('devices')}: {k} {part}",
-                        sp[k].get(part, {}).get("score"), refs.get((Ls, sp[k]["score_bits"])))
+                    r = sp[k].get(part, {})
+                    name = f"split over devices {devs}: {k} {part}"
+                    if cross and part == "split" and r.get("score") is None:
+                        errors[name] = r.get("error", "no score")
+                        continue
+                    put(name, r.get("score"), refs.get((Ls, sp[k]["score_bits"])))
         # the reference's own parity input: dat/{A,B,C}_seq.dat through tsa_score_gpu
         with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
             dat = next(c for c in json.load(f)["cases"] if c["name"] == "dat")
@@ -553,6 +568,8 @@ def oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single, pending)
         n_bad = len(bad) + sum(not c["ok"] for c in configs.values())
         parity = {"mismatches": n_bad, "batch": batch, "configs": configs,
                   "against": "oracle/tsa_oracle.c (literal RTL form, same inputs)"}
+        if errors:
+            parity["errors"] = errors
         if world == 1 and not args.no_cpu_baseline:
             # bounded sample of the same workload: one L^3 triple per thread per round
             t_one = oracle.now()

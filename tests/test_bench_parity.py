@@ -1,0 +1,58 @@
+"""bench.py's parity leg (oracle_leg) on the CPU: the per-config {gpu, oracle,
+ok} records, and how the split-over-devices leg counts. GPU scores are stood in
+by the oracle's own (this checks the bookkeeping, not a kernel)."""
+import os
+import sys
+from argparse import Namespace
+from concurrent.futures import Future
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _done(v):
+    f = Future()
+    f.set_result(v)
+    return f
+
+
+def _leg(tsa, orc, synth, split):
+    import bench
+    L, n = 16, 6
+    ref = {i: orc.score(*synth.triple(i, L), orc.default_params(score_bits=12)) for i in range(n)}
+
+    class GpuStandIn:
+        pack_batch = staticmethod(tsa.pack_batch)
+
+        @staticmethod
+        def score(a, b, c, device=0):
+            return orc.score(a, b, c)
+
+    args = Namespace(check=3, score_bits=12, no_extra_configs=True, no_cpu_baseline=True, cpu_seconds=1)
+    single = {f"configs[2]: {L}^3": {"score": ref[0]}, "split over devices": split}
+    scores = np.array([ref[i] for i in range(n)], dtype=np.int32)
+    parity, _ = bench.oracle_leg(args, GpuStandIn, synth, 1, n, L, scores, single, {(L, 12): _done(ref[0])})
+    return parity, ref[0]
+
+
+def test_parity_leg_counts_configs_and_split(tsa, orc, synth):
+    ok = lambda s: {"parts": 1, "us": 1.0, "score": s}  # noqa: E731
+    # one GPU: both split scores checked; an error there is a mismatch
+    parity, s0 = _leg(tsa, orc, synth, {"devices": [0, 0], "16^3": {"score_bits": 12, "one_part": ok(None), "split": ok(None)}})
+    assert parity["mismatches"] == 2 and "errors" not in parity
+    parity, s0 = _leg(tsa, orc, synth, {"devices": [0, 0], "16^3": {"score_bits": 12, "one_part": ok(s0), "split": ok(s0)}})
+    assert parity["mismatches"] == 0 and parity["batch"]["checked"] >= 3
+    assert parity["configs"]["configs[0]: dat/{A,B,C}_seq.dat (tsa_score_gpu)"]["ok"]
+    # distinct GPUs: a wrong split score fails, an error (no score) is recorded
+    # under errors without failing the line
+    parity, _ = _leg(tsa, orc, synth, {"devices": [0, 1], "16^3": {"score_bits": 12, "one_part": ok(s0), "split": ok(s0 + 1)}})
+    assert parity["mismatches"] == 1
+    parity, _ = _leg(tsa, orc, synth, {"devices": [0, 1], "16^3": {"score_bits": 12, "one_part": ok(s0),
+                                                                  "split": {"parts": 2, "error": "peer access"}}})
+    assert parity["mismatches"] == 0 and list(parity["errors"].values()) == ["peer access"]
+    parity, _ = _leg(tsa, orc, synth, {"devices": "0,1", "error": "rc=1: boom"})
+    assert parity["mismatches"] == 0 and parity["errors"] == {"split over devices": "rc=1: boom"}
+    parity, _ = _leg(tsa, orc, synth, {"devices": "0,0", "error": "rc=1: boom"})
+    assert parity["mismatches"] == 1
