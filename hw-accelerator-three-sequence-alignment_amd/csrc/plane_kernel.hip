@@ -20,7 +20,8 @@
 // plane q: it stages the tile plus a one-row / one-column halo of planes q-1,
 // q-2 and q-3 -- every predecessor its cells need -- in LDS with coalesced
 // 16-byte loads (3 (TY+1) 65 cells, ~4 loads per thread instead of 49 2-byte
-// gathers per cell), then each cell reads its 7 predecessors as 7 ds_read_b128.
+// gathers per cell); each cell reads its own column's 5 predecessors from LDS
+// and takes the 4 at z-1 from its left lane by DPP (a wave = one tile row).
 //
 // This kernel is the exact path for every parameter set and length (the
 // pencil kernel's factored arithmetic is exact only when nothing wraps).
@@ -138,6 +139,14 @@ __device__ __forceinline__ void pairs7(uint4 c, uint32_t (&p)[4]) {
   p[3] = (c.w & 0xFFFFu) * 0x00010001u;
 }
 
+// Lane l <- lane l-1 of a 16-byte cell (DPP wave_shr:1); lane 0 keeps `halo`.
+__device__ __forceinline__ uint32_t shr1_u32(uint32_t v, uint32_t halo) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)halo, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint4 lane_shr1(uint4 v, uint4 halo) {
+  return make_uint4(shr1_u32(v.x, halo.x), shr1_u32(v.y, halo.y), shr1_u32(v.z, halo.z), shr1_u32(v.w, halo.w));
+}
+
 // Traceback pointer cube index of cell (x,y,z), 1-based: [y-1][x+z-2][z-1].
 __host__ __device__ inline int64_t tb_index(int32_t x, int32_t y, int32_t z, int32_t la,
                                             int32_t lc) {
@@ -178,6 +187,29 @@ __global__ __launch_bounds__(64 * PLANE_TY) void plane_step_kernel(
   __syncthreads();
 
   const int32_t y = y0 + (int32_t)threadIdx.y, z = z0 + (int32_t)threadIdx.x;
+  // A wave is one row of the tile (64 consecutive z): each lane reads its own
+  // column of the staged planes, and the z-1 predecessors come from lane - 1
+  // by DPP (wave_shr:1) -- lane 0 takes the staged halo column z0 - 1. Every
+  // lane of the row reads before any returns: a lane whose own cell is off the
+  // plane still hands its column to lane + 1.
+  const int r = (int)threadIdx.y + 1, c = (int)threadIdx.x + 1;  // staged row / column of (y, z)
+  const uint4 *T1 = tile, *T2 = tile + PLANE_TILE, *T3 = tile + 2 * PLANE_TILE;
+  const uint4 cX = T1[r * PLANE_TW + c];             // (x-1,y,  z  )  Ix   src/PE_1cyc.v:172-178
+  const uint4 cY = T1[(r - 1) * PLANE_TW + c];       // (x,  y-1,z  )  Iy   :180-186
+  const uint4 cXY = T2[(r - 1) * PLANE_TW + c];      // (x-1,y-1,z  )  Ixy  :196-202
+  const uint4 oXZ = T2[r * PLANE_TW + c];            // lane + 1's Ixz predecessor
+  const uint4 oM = T3[(r - 1) * PLANE_TW + c];       // lane + 1's M predecessor
+  uint4 hZ = make_uint4(0u, 0u, 0u, 0u), hYZ = hZ, hXZ = hZ, hM = hZ;
+  if (threadIdx.x == 0) {  // the halo column
+    hZ = T1[r * PLANE_TW];
+    hYZ = T2[(r - 1) * PLANE_TW];
+    hXZ = T2[r * PLANE_TW];
+    hM = T3[(r - 1) * PLANE_TW];
+  }
+  const uint4 cZ = lane_shr1(cX, hZ);     // (x,  y,  z-1)  Iz   :188-194
+  const uint4 cYZ = lane_shr1(cXY, hYZ);  // (x,  y-1,z-1)  Iyz  :204-210
+  const uint4 cXZ = lane_shr1(oXZ, hXZ);  // (x-1,y,  z-1)  Ixz  :212-218
+  const uint4 cM = lane_shr1(oM, hM);     // (x-1,y-1,z-1)  M    :164-170
   if (y > yhi || z < max(1, q - la - y) || z > min(lc, q - y)) return;
   const int32_t x = q - y - z;
   uint4 *out = base + (int64_t)(q & 3) * P + (int64_t)y * L.ldz + z;
@@ -185,15 +217,6 @@ __global__ __launch_bounds__(64 * PLANE_TY) void plane_step_kernel(
     *out = make_uint4(0u, 0u, 0u, 0u);
     return;
   }
-  const int r = (int)threadIdx.y + 1, c = (int)threadIdx.x + 1;  // staged row / column of (y, z)
-  const uint4 *T1 = tile, *T2 = tile + PLANE_TILE, *T3 = tile + 2 * PLANE_TILE;
-  const uint4 cM = T3[(r - 1) * PLANE_TW + c - 1];   // (x-1,y-1,z-1)  M    src/PE_1cyc.v:164-170
-  const uint4 cX = T1[r * PLANE_TW + c];             // (x-1,y,  z  )  Ix   :172-178
-  const uint4 cY = T1[(r - 1) * PLANE_TW + c];       // (x,  y-1,z  )  Iy   :180-186
-  const uint4 cZ = T1[r * PLANE_TW + c - 1];         // (x,  y,  z-1)  Iz   :188-194
-  const uint4 cXY = T2[(r - 1) * PLANE_TW + c];      // (x-1,y-1,z  )  Ixy  :196-202
-  const uint4 cYZ = T2[(r - 1) * PLANE_TW + c - 1];  // (x,  y-1,z-1)  Iyz  :204-210
-  const uint4 cXZ = T2[r * PLANE_TW + c - 1];        // (x-1,y,  z-1)  Ixz  :212-218
   const int a = tsa_sym(seqs, o0 + x - 1, kp.packed), b = tsa_sym(seqs, o1 + y - 1, kp.packed),
             cc = tsa_sym(seqs, o2 + z - 1, kp.packed);
   const int32_t sh = kp.wrap_shift;
