@@ -301,7 +301,7 @@ def report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gc
     # kernel, arithmetic and schedule the library picks (host-only query)
     plan = tsa.describe_plan(max(per_gpu, 1), L, L, L, params, kernel=kind, sync=False)
     # exact integer values in f16 / int16 lanes; plane: int32 math on int16 planes
-    arith = "f16" if " f16" in plan else ("i32" if plan == "plane" else "i16")
+    arith = "f16" if " f16" in plan else ("i32" if plan.split()[:2] == ["plane", "est"] else "i16")
 
     per_gpu_cells = n * L * L * L
     kernel_s = kernel_ms_per_step * 1e-3

@@ -27,8 +27,12 @@ struct LapGeom {
   int64_t blocks;    // grid (padding blocks for the XCD-aware tile mapping)
   size_t lds, prog_bytes, yf_bytes, zf_bytes, yb_bytes, zb_bytes;
   int64_t waves;     // dispatch rounds: 1 = every workgroup resident at once
-  double est_us;     // estimated latency
+  double est_us;     // estimated latency (lap_geom_chunked: of every launch)
   bool ok;           // feasible and more than one workgroup per triple
+  // lap_geom_chunked: a batch runs as launches of `chunk` triples, one after
+  // another on the stream (0: one launch); the geometry above is a chunk's
+  int32_t chunk;
+  int32_t max_la, max_lb, max_lc;
 };
 
 // A grid beyond the resident slots runs in dispatch rounds (boundary rings
@@ -41,6 +45,13 @@ constexpr int64_t LAP_MAX_WAVES = 3;
 // lit: the literal form (lap_kernel LIT: int16 shifted words, M <= 2).
 LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW,
                  bool full_rings, bool f16, bool sop, bool lit = false);
+// A batch of n triples as sequential launches of `chunk` triples each, so
+// that every launch's grid keeps to the dispatch-round rules (at most
+// LAP_MAX_WAVES rounds, one workgroup per CU when there are several): the
+// chunk of least total estimated latency (TSA_LAP_CHUNK forces one, tests).
+// .ok = false when no chunk size fits.
+LapGeom lap_geom_chunked(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW, bool f16,
+                         bool sop, bool lit = false);
 size_t lap_workspace_bytes(const LapGeom &g);
 // The launch's error word inside a workspace of n triples (set on a hand-off timeout).
 uint32_t *lap_err_word(const LapGeom &g, int32_t n, void *d_ws);

@@ -1313,17 +1313,16 @@ static int lap_blocks_per_cu_lit(size_t lds) {
   ((M_) == 1 ? ((NW_) == 4 ? TSA_LIT_SOP(FN, 1, 4, SOP_, __VA_ARGS__) : TSA_LIT_SOP(FN, 1, 8, SOP_, __VA_ARGS__)) \
              : ((NW_) == 4 ? TSA_LIT_SOP(FN, 2, 4, SOP_, __VA_ARGS__) : TSA_LIT_SOP(FN, 2, 8, SOP_, __VA_ARGS__)))
 
-// Step time (us) along the chain, fitted to single-cube runs on MI355X
-// (scripts/gpu_lapvar.sh, tools/lap_trace.py): 64^3..512^3 at
-// M = 1 give 0.34-0.45 (NW = 4) and 0.42-0.48 (NW = 8), growing with the
-// workgroups per CU; M = 2 / 4 carry the round-1 fits scaled the same way --
-// the chain steps include the hand-off stalls.
-// LIT: the literal cell's step, 1.3-1.5x the message form's (single cubes
-// 64^3 .. 1024^3 on MI355X, profiles/r3l_literal_lap_vs_plane.jsonl against
-// the r3h bench's lap timings).
+// Step time (us) along the chain, fitted on MI355X to single cubes
+// (scripts/gpu_lapvar.sh, tools/lap_trace.py; DESIGN.md 4.4: 64^3..1024^3
+// within ~10 %) and to batches of 4..128 cubes (profiles/r3o_chunk.jsonl:
+// M = 4, 16 x 256^3 .. 4 x 1024^3), growing with the workgroups per CU -- the
+// chain steps include the hand-off stalls.
+// LIT: the literal cell's step, ~1.6x the message form's (single cubes and
+// batches, profiles/r3l_literal_lap_vs_plane.jsonl, r3o_chunk.jsonl).
 static double lap_step_us(int M, int NW, int64_t wg_per_cu, bool lit = false) {
-  const double base = M == 1 ? (NW == 4 ? 0.36 : 0.44) : M == 2 ? 0.55 : 0.72;
-  return (lit ? 1.45 : 1.0) * base * (1.0 + 0.22 * (double)(std::max<int64_t>(wg_per_cu, 1) - 1));
+  const double base = M == 1 ? (NW == 4 ? 0.40 : 0.49) : M == 2 ? 0.62 : 1.45;
+  return (lit ? 1.6 : 1.0) * base * (1.0 + 0.22 * (double)(std::max<int64_t>(wg_per_cu, 1) - 1));
 }
 
 LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW,
@@ -1334,6 +1333,10 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   LapGeom g{};
   g.M = M;
   g.NW = NW;
+  g.chunk = 0;
+  g.max_la = max_la;
+  g.max_lb = max_lb;
+  g.max_lc = max_lc;
   const int RW = 2 * NW, ZT = 64 * M, LPD = lap_pd(M);
   g.G = (max_lb + RW - 1) / RW;
   g.GZ = (max_lc + ZT - 1) / ZT;
@@ -1414,6 +1417,30 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   return g;
 }
 
+LapGeom lap_geom_chunked(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW, bool f16,
+                         bool sop, bool lit) {
+  LapGeom best{};
+  best.ok = false;
+  int32_t forced = 0;
+  if (const char *e = getenv("TSA_LAP_CHUNK")) forced = std::max(0, atoi(e));  // knob (tests)
+  // chunk sizes n, ceil(n/2), ceil(n/4), .. 1: a later launch starts once
+  // the earlier one drains (~5 us between launches on one stream)
+  for (int32_t k = n;; k = (k + 1) / 2) {
+    const int32_t kk = forced > 0 ? std::min(forced, n) : k;
+    LapGeom g = lap_geom(kk, max_la, max_lb, max_lc, M, NW, false, f16, sop, lit);
+    // rounds with two workgroups per CU: a later round's workgroups start out
+    // of chain order as slots free (lap_choice)
+    if (g.ok && g.waves <= LAP_MAX_WAVES && !(g.waves > 1 && g.per_cu > 1)) {
+      const int64_t launches = (n + kk - 1) / kk;
+      g.chunk = kk < n ? kk : 0;
+      g.est_us = g.est_us * (double)launches + 5.0 * (double)(launches - 1);
+      if (!best.ok || g.est_us < best.est_us) best = g;
+    }
+    if (forced > 0 || k == 1) break;
+  }
+  return best;
+}
+
 size_t lap_workspace_bytes(const LapGeom &g) {
   return g.prog_bytes + g.yf_bytes + g.zf_bytes + g.yb_bytes + g.zb_bytes;
 }
@@ -1421,8 +1448,12 @@ static LapRounds lap_rounds(const LapGeom &g, void *d_ws) {
   uint8_t *yb = (uint8_t *)d_ws + g.prog_bytes + g.yf_bytes + g.zf_bytes;
   return LapRounds{g.SX, g.KBY, g.YRB, g.ZRB, yb, yb + g.yb_bytes};
 }
+// The error word sits after the progress words of the workgroups the
+// geometry was built for (NC * G; one chunk's, whatever the batch size), the
+// checked kernel's monitor words 64 words further.
 uint32_t *lap_err_word(const LapGeom &g, int32_t n, void *d_ws) {
-  return (uint32_t *)((int32_t *)d_ws + (int64_t)n * g.G * g.GZ * LAP_PROG_STRIDE);
+  (void)n;
+  return (uint32_t *)((int32_t *)d_ws + (int64_t)g.NC * g.G * LAP_PROG_STRIDE);
 }
 
 static uint32_t lap_spin_limit() {
@@ -1439,22 +1470,32 @@ static uint32_t lap_next_epoch() {
 typedef decltype(&lap_kernel<1, 4, true, false, false>) LapKernelFn;  // every instantiation's type
 // aux: the checked kernel's monitor words (chk), or the LIT kernel's final
 // 7-tuples (may be null)
+// One launch of n triples on geometry g (built for n) inside the workspace
+// of the allocation geometry ga (the batch's chunk geometry; g itself for a
+// single launch): every region at ga's offset -- progress words, y / z rings,
+// boundary rings -- and the error word / the checked kernel's monitor words at
+// ga's place (lap_err_word), the same for every chunk of a batch.
 static int launch_lap_fn(LapKernelFn kfn, int NW, const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
-                         const LapGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
-                         const LitArgs &lit, int32_t *aux, hipStream_t stream, const CheckLimits *chk) {
+                         const LapGeom &g, const LapGeom &ga, int32_t *d_scores, void *d_ws,
+                         const PencilArgs &pa, const LitArgs &lit, int32_t *aux, hipStream_t stream,
+                         const CheckLimits *chk) {
   if (g.lds > LDS_MAX) return TSA_EINVAL;
+  if (g.prog_bytes > ga.prog_bytes || g.yf_bytes > ga.yf_bytes || g.zf_bytes > ga.zf_bytes ||
+      g.yb_bytes > ga.yb_bytes || g.zb_bytes > ga.zb_bytes)
+    return TSA_EINTERNAL;  // a chunk's regions must fit the batch's
   if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)g.lds) != hipSuccess)
     return TSA_EDEVICE;
   int32_t *prog = (int32_t *)d_ws;
-  const int64_t wgs = (int64_t)n * g.G * g.GZ;
-  uint32_t *err = (uint32_t *)(prog + wgs * LAP_PROG_STRIDE);
-  int32_t *mon = chk ? prog + wgs * LAP_PROG_STRIDE + 64 : aux;  // [max(best)] n, [min(best)] n
+  uint32_t *err = lap_err_word(ga, n, d_ws);
+  int32_t *mon = chk ? (int32_t *)err + 64 : aux;  // [max(best)] n, [min(best)] n
   if (chk && (hipMemsetAsync(mon, 0x80, (size_t)n * 4, stream) != hipSuccess ||
               hipMemsetAsync(mon + n, 0x7F, (size_t)n * 4, stream) != hipSuccess))
     return TSA_EDEVICE;
-  uint8_t *yf = (uint8_t *)d_ws + g.prog_bytes;
-  uint8_t *zf = yf + g.yf_bytes;
+  uint8_t *yf = (uint8_t *)d_ws + ga.prog_bytes;
+  uint8_t *zf = yf + ga.yf_bytes;
+  uint8_t *yb = zf + ga.zf_bytes;
+  const LapRounds rd{g.SX, g.KBY, g.YRB, g.ZRB, yb, yb + ga.yb_bytes};
   unsigned long long *trace = nullptr;
   const char *tpath = getenv("TSA_LAP_TRACE");  // diagnostic: per-WG timestamps to a CSV file
   const size_t tbytes = (size_t)g.blocks * LAP_TRACE_SLOTS * 8;
@@ -1463,7 +1504,7 @@ static int launch_lap_fn(LapKernelFn kfn, int NW, const uint8_t *d_seqs, const i
     return TSA_EDEVICE;
   const uint32_t epoch = lap_next_epoch();
   hipLaunchKernelGGL(kfn, dim3((uint32_t)g.blocks), dim3(64 * (NW + 1)), g.lds, stream, d_seqs,
-                     d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, lap_rounds(g, d_ws), prog, err,
+                     d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, rd, prog, err,
                      d_scores, mon, pa,
                      epoch, lap_spin_limit(), 0, g.G, yf, prog, trace, lit);
   if (chk) {
@@ -1499,20 +1540,41 @@ static int launch_lap_fn(LapKernelFn kfn, int NW, const uint8_t *d_seqs, const i
   }
   return TSA_OK;
 }
+// A batch on geometry g: one launch, or (g.chunk) launches of g.chunk
+// triples one after another on the stream, each with its own epoch; the last
+// chunk's geometry is built for its own size, inside g's workspace.
+template <class F>
+static int for_each_chunk(const LapGeom &g, int32_t n, bool f16, bool sop, bool lit, F &&launch) {
+  const int32_t k = (g.chunk > 0 && g.chunk < n) ? g.chunk : n;
+  for (int32_t c0 = 0; c0 < n; c0 += k) {
+    const int32_t cn = std::min(k, n - c0);
+    const LapGeom gc = cn == k ? g : lap_geom(cn, g.max_la, g.max_lb, g.max_lc, g.M, g.NW, false, f16, sop, lit);
+    if (!gc.ok && cn != k) return TSA_EINTERNAL;
+    const int rc = launch(gc, c0, cn);
+    if (rc) return rc;
+  }
+  return TSA_OK;
+}
 template <int M, int NW, bool F16, bool SOP>
 static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                       const LapGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
                       hipStream_t stream, const CheckLimits *chk) {
   if (chk && F16) return TSA_EINVAL;
   auto kfn = chk ? lap_kernel<M, NW, F16, SOP, !F16> : lap_kernel<M, NW, F16, SOP, false>;
-  return launch_lap_fn(kfn, NW, d_seqs, d_offsets, n, g, d_scores, d_ws, pa, LitArgs{}, nullptr, stream, chk);
+  return for_each_chunk(g, n, F16, SOP, false, [&](const LapGeom &gc, int32_t c0, int32_t cn) {
+    return launch_lap_fn(kfn, NW, d_seqs, d_offsets + 3 * (int64_t)c0, cn, gc, g, d_scores + c0, d_ws, pa,
+                         LitArgs{}, nullptr, stream, chk);
+  });
 }
 template <int M, int NW, bool SOP>
 static int launch_lap_lit(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, const LapGeom &g,
                           int32_t *d_scores, int32_t *d_final7, void *d_ws, const PencilArgs &pa,
                           const LitArgs &lit, hipStream_t stream) {
-  return launch_lap_fn(lap_kernel<M, NW, false, SOP, false, false, true>, NW, d_seqs, d_offsets, n, g, d_scores,
-                       d_ws, pa, lit, d_final7, stream, nullptr);
+  return for_each_chunk(g, n, false, SOP, true, [&](const LapGeom &gc, int32_t c0, int32_t cn) {
+    return launch_lap_fn(lap_kernel<M, NW, false, SOP, false, false, true>, NW, d_seqs, d_offsets + 3 * (int64_t)c0,
+                         cn, gc, g, d_scores + c0, d_ws, pa, lit, d_final7 ? d_final7 + 7 * (int64_t)c0 : nullptr,
+                         stream, nullptr);
+  });
 }
 
 int lap_launch_lit(const LapGeom &g, bool sop, const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
@@ -1520,7 +1582,7 @@ int lap_launch_lit(const LapGeom &g, bool sop, const uint8_t *d_seqs, const int6
                    int32_t **d_err) {
   if (g.M > 2 || (g.NW != 4 && g.NW != 8)) return TSA_EINVAL;
   if (d_err) {  // synchronous caller: clear the error word, it reads it back
-    *d_err = (int32_t *)d_ws + (int64_t)n * g.G * g.GZ * LAP_PROG_STRIDE;
+    *d_err = (int32_t *)lap_err_word(g, n, d_ws);
     if (hipMemsetAsync(*d_err, 0, sizeof(int32_t), stream) != hipSuccess) return TSA_EDEVICE;
   }
   PencilArgs pa{};  // the literal form reads only the packed flag; zero faces
@@ -1535,7 +1597,7 @@ int lap_launch(const LapGeom &g, bool f16, bool sop, const uint8_t *d_seqs,
                const PencilArgs &pa, hipStream_t stream, int32_t **d_err,
                const CheckLimits *chk) {
   if (d_err) {  // synchronous caller: clear the error word, it reads it back
-    *d_err = (int32_t *)d_ws + (int64_t)n * g.G * g.GZ * LAP_PROG_STRIDE;
+    *d_err = (int32_t *)lap_err_word(g, n, d_ws);
     if (hipMemsetAsync(*d_err, 0, sizeof(int32_t), stream) != hipSuccess) return TSA_EDEVICE;
   }
   return TSA_LAP_SHAPES(launch_lap, g.M, g.NW, f16, sop, d_seqs, d_offsets, n, g, d_scores, d_ws,

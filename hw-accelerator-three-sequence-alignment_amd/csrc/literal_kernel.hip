@@ -86,8 +86,8 @@ static LapGeom literal_lap_choice(int32_t n, int32_t max_la, int32_t max_lb, int
   if (const char *e = getenv("TSA_LAP_NW")) nw_lo = nw_hi = atoi(e) == 4 ? 4 : 8;
   for (int M = m_lo; M <= m_hi; M *= 2)
     for (int NW = nw_lo; NW <= nw_hi; NW *= 2) {
-      const LapGeom g = lap_geom(n, max_la, max_lb, max_lc, M, NW, false, false, sop, true);
-      if (!g.ok || g.waves > LAP_MAX_WAVES || (g.waves > 1 && g.per_cu > 1)) continue;  // as lap_choice
+      const LapGeom g = lap_geom_chunked(n, max_la, max_lb, max_lc, M, NW, false, sop, true);  // as lap_choice
+      if (!g.ok) continue;
       if (!best.ok || g.est_us < best.est_us) best = g;
     }
   return best;
@@ -106,7 +106,7 @@ int literal_kind(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, bool
     if (h <= best) { best = h; kind = LIT_HELIX; }
   }
   const LapGeom g = literal_lap_choice(n, max_la, max_lb, max_lc, sop, lap);
-  if (g.ok && g.est_us < best) kind = LIT_LAP;
+  if (g.ok && 1.25 * g.est_us < best) kind = LIT_LAP;  // by a margin, as lap_choice
   return kind;
 }
 bool literal_helix_chosen(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc) {
@@ -589,8 +589,12 @@ void literal_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
     const LapGeom g = literal_lap_choice(n, max_la, max_lb, max_lc, sop, lap);
     snprintf(buf, len, "plane literal-lap M=%d NW=%d laps=%d tiles=%d waves=%lld", g.M, g.NW, g.G, g.GZ,
              (long long)g.waves);
+    if (g.chunk > 0) snprintf(buf + strlen(buf), len - strlen(buf), " chunk=%d", g.chunk);
+    snprintf(buf + strlen(buf), len - strlen(buf), " est=%.0fus", g.est_us);
+  } else if (kind == LIT_HELIX) {
+    snprintf(buf, len, "plane literal-helix est=%.0fus", literal_helix_us(n, max_la, max_lb, max_lc));
   } else {
-    snprintf(buf, len, kind == LIT_HELIX ? "plane literal-helix" : "plane");
+    snprintf(buf, len, "plane est=%.0fus", plane_us(n, max_la, max_lb, max_lc));
   }
 }
 

@@ -156,19 +156,22 @@ static LapGeom lap_choice(int32_t n, int32_t max_la, int32_t max_lb, int32_t max
     for (int NW = nw_lo; NW <= nw_hi; NW *= 2) {
       // a grid of several dispatch rounds runs with boundary rings (lap_geom)
       // on both paths: it relies on per-XCD in-order dispatch, measured
-      // (DESIGN.md 4.4); a hand-off that times out still reports, never hangs
-      const LapGeom g = lap_geom(n, max_la, max_lb, max_lc, M, NW, false, f16, sop);
-      if (!g.ok || g.waves > LAP_MAX_WAVES) continue;
-      // rounds with two workgroups per CU: a later round's workgroups start out
-      // of chain order as slots free, lags reach ~1100 steps and the slim rings
-      // stall (1024^3 M = 1 NW = 8: 37206 back-pressure waits, timed out);
-      // with one per CU they start in chain order (M = 2: none, 3.00 ms)
-      if (g.waves > 1 && g.per_cu > 1) continue;
+      // (DESIGN.md 4.4); a hand-off that times out still reports, never hangs.
+      // Rounds with two workgroups per CU are refused (a later round's
+      // workgroups start out of chain order as slots free, lags reach ~1100
+      // steps and the slim rings stall: 1024^3 M = 1 NW = 8, 37206
+      // back-pressure waits, timed out; with one per CU they start in chain
+      // order, M = 2: none, 3.00 ms); a larger batch runs as chunks of
+      // triples, one launch each (lap_geom_chunked)
+      const LapGeom g = lap_geom_chunked(n, max_la, max_lb, max_lc, M, NW, f16, sop);
+      if (!g.ok) continue;
       if (!best.ok || g.est_us < best.est_us) best = g;
     }
   }
-  // `need` (the checked kernel): the lap schedule whatever the helix would cost
-  if (best.ok && !force && !need && best.est_us >= helix_est(n, max_la, max_lb, max_lc)) return none;
+  // `need` (the checked kernel): the lap schedule whatever the helix would cost;
+  // otherwise the lap must win by a margin (its estimate is ~10-30 % uncertain,
+  // and the helix has no cross-workgroup dependency)
+  if (best.ok && !force && !need && 1.25 * best.est_us >= helix_est(n, max_la, max_lb, max_lc)) return none;
   return best;
 }
 
@@ -860,14 +863,16 @@ void pencil_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, 
   const char *s3 = kp.s3_mode == TSA_S3_SOP ? "sop" : "rtl";
   const LapGeom lg = lap_choice(n, max_la, max_lb, max_lc, lap, f16, kp.s3_mode == TSA_S3_SOP, checked);
   if (lg.ok) {
-    snprintf(buf, len, "pencil lap %s %s M=%d NW=%d laps=%d tiles=%d waves=%lld%s", arith, s3, lg.M,
-             lg.NW, lg.G, lg.GZ, (long long)lg.waves, checked ? " checked" : "");
+    char chunk[32] = "";
+    if (lg.chunk > 0) snprintf(chunk, sizeof chunk, " chunk=%d", lg.chunk);
+    snprintf(buf, len, "pencil lap %s %s M=%d NW=%d laps=%d tiles=%d waves=%lld%s%s est=%.0fus", arith, s3, lg.M,
+             lg.NW, lg.G, lg.GZ, (long long)lg.waves, chunk, checked ? " checked" : "", lg.est_us);
     return;
   }
   const PencilGeom g = pencil_geom(max_la, max_lc);
   if (use_vs(kp, bound, max_la, max_lb, max_lc)) arith = "f16v";  // the helix's V-space cell
-  snprintf(buf, len, "pencil helix %s %s M=%d NW=%d P=%d%s", arith, s3, g.M, helix_nw(g.M), g.P,
-           g.two ? " two" : "");
+  snprintf(buf, len, "pencil helix %s %s M=%d NW=%d P=%d%s est=%.0fus", arith, s3, g.M, helix_nw(g.M), g.P,
+           g.two ? " two" : "", helix_est(n, max_la, max_lb, max_lc));
 }
 
 int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,

@@ -101,17 +101,23 @@ def test_describe_plan(tsa):
                              ).startswith("pencil helix f16 rtl")
     assert tsa.describe_plan(512, 400, 400, 400, p).startswith("pencil helix f16 rtl M=4")
     assert tsa.describe_plan(1, 256, 256, 256, p).startswith("pencil lap f16 rtl M=1")
-    # a few cubes: the lap kernel; many: the helix; the synchronous path may
-    # stream a lap grid beyond the resident slots (waves > 1), the async one not
+    # a few cubes: the lap kernel; many: the helix; a batch beyond the lap
+    # grid's dispatch-round rules runs as chunks of triples, one launch each
     assert tsa.describe_plan(4, 256, 256, 256, p, sync=False).startswith("pencil lap f16")
-    assert tsa.describe_plan(64, 256, 256, 256, p, sync=False).startswith("pencil helix")
+    assert tsa.describe_plan(128, 256, 256, 256, p, sync=False).startswith("pencil helix")
+    assert " chunk=4 " in tsa.describe_plan(8, 512, 512, 512, p, sync=False)
+    assert tsa.describe_plan(64, 1024, 1024, 1024, tsa.TsaParams.default(score_bits=16)).startswith("pencil helix")
     import os
     os.environ["TSA_PENCIL_MODE"] = "lap"
     try:
-        assert "waves=1" not in tsa.describe_plan(100, 129, 128, 128, p, sync=True)
-        assert tsa.describe_plan(100, 129, 128, 128, p, sync=False).startswith("pencil helix")
+        for sync in (True, False):
+            plan = tsa.describe_plan(100, 129, 128, 128, p, sync=sync)
+            assert plan.startswith("pencil lap") and " chunk=" in plan, plan
+        os.environ["TSA_LAP_CHUNK"] = "7"
+        assert " chunk=7 " in tsa.describe_plan(100, 129, 128, 128, p, sync=False)
     finally:
         del os.environ["TSA_PENCIL_MODE"]
+        os.environ.pop("TSA_LAP_CHUNK", None)
     # M = 2 lap periods are even (the x = 1 register is then PH ^ (w & 1))
     assert "M=2 NW=8 P=258" in tsa.describe_plan(512, 257, 40, 255, p)
     assert "M=2 NW=8 P=256" in tsa.describe_plan(512, 255, 40, 255, p)
@@ -123,20 +129,21 @@ def test_describe_plan(tsa):
     # (lap_kernel LIT), the literal helix for batches, the plane sweep where
     # neither runs (many cubes with LC > 512)
     assert tsa.describe_plan(4, 64, 64, 64, p, kernel="plane").startswith("plane literal-lap M=1")
-    assert tsa.describe_plan(512, 256, 256, 256, p, kernel="plane") == "plane literal-helix"
+    assert tsa.describe_plan(512, 256, 256, 256, p, kernel="plane").startswith("plane literal-helix")
     assert tsa.describe_plan(1, 256, 256, 256, p, kernel="plane").startswith("plane literal-lap")
     assert tsa.describe_plan(1, 1024, 1024, 1024, p, kernel="plane").startswith("plane literal-lap M=2 NW=8")
-    assert tsa.describe_plan(64, 1024, 1024, 1024, p, kernel="plane") == "plane"
+    assert tsa.describe_plan(64, 1024, 1024, 1024, p, kernel="plane").startswith("plane literal-lap")
+    assert tsa.describe_plan(4096, 1024, 1024, 1024, p, kernel="plane").startswith("plane literal-lap")
     # without the lap schedule (the helix / sweep rescue of a timed-out lap)
     os.environ["TSA_PENCIL_MODE"] = "literal"
     try:
-        assert tsa.describe_plan(4, 64, 64, 64, p, kernel="plane") == "plane literal-helix"
+        assert tsa.describe_plan(4, 64, 64, 64, p, kernel="plane").startswith("plane literal-helix")
     finally:
         del os.environ["TSA_PENCIL_MODE"]
     # gap_extend > gap_open: the widened message groups are not exact -> literal
     ge = tsa.TsaParams.default(gap_open=1, gap_extend=2)
     assert tsa.describe_plan(4, 64, 64, 64, ge).startswith("plane literal-lap")
-    assert tsa.describe_plan(512, 64, 64, 64, ge) == "plane literal-helix"
+    assert tsa.describe_plan(512, 64, 64, 64, ge).startswith("plane literal-")
     with pytest.raises(tsa.TsaError) as e:
         tsa.describe_plan(4, 64, 64, 64, ge, kernel="pencil")
     assert e.value.rc == tsa.TSA_ERANGE
@@ -145,12 +152,13 @@ def test_describe_plan(tsa):
     # whatever it cannot certify), and so does an explicit kernel="checked"
     p6 = tsa.TsaParams.default(score_bits=6)
     assert tsa.describe_plan(4, 90, 90, 90, p6, sync=False).startswith("plane literal-lap")
-    assert tsa.describe_plan(4, 90, 90, 90, p6, sync=True).endswith(" checked")
+    assert tsa.describe_plan(4, 90, 90, 90, p6, sync=True).split(" est=")[0].endswith(" checked")
     assert tsa.describe_plan(1, 1024, 1024, 1024, p, sync=True).startswith("pencil lap i16 rtl")
     assert tsa.describe_plan(1, 1024, 1024, 1024, p, sync=False).startswith("plane literal-lap M=2 NW=8")
-    assert tsa.describe_plan(1, 1024, 1024, 1024, p, kernel="checked", sync=False).endswith(" checked")
-    # a batch too large for the lap schedule is never checked
-    assert tsa.describe_plan(4096, 800, 800, 800, p, sync=True) == "plane"
+    assert tsa.describe_plan(1, 1024, 1024, 1024, p, kernel="checked", sync=False).split(" est=")[0].endswith(" checked")
+    # a large batch is checked in chunks of the lap schedule
+    plan = tsa.describe_plan(4096, 800, 800, 800, p, sync=True)
+    assert plan.startswith("pencil lap i16") and " chunk=" in plan and " checked" in plan, plan
 
 
 def test_lap_rounds_and_ring_memory(tsa):

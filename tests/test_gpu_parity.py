@@ -534,7 +534,7 @@ def test_checked_1024_rtl_words(gpu, orc, synth):
     L = 1024
     a, b, c = synth.triple(5, L)
     p = gpu.TsaParams.default()
-    assert gpu.describe_plan(1, L, L, L, p, sync=True).endswith(" checked")
+    assert gpu.describe_plan(1, L, L, L, p, sync=True).split(" est=")[0].endswith(" checked")
     before = gpu.check_fallback_count()
     got = gpu.score(a, b, c, p)
     assert got == orc.score(a, b, c, orc.default_params())
@@ -573,7 +573,7 @@ def test_checked_narrow_words_batch(gpu, orc):
         triples = [tuple(rng.integers(0, 4, n).astype(np.uint8) for n in (90, 70, 100))
                    for _ in range(3)]
         p, op = gpu.TsaParams.default(score_bits=bits), orc.default_params(score_bits=bits)
-        assert gpu.describe_plan(3, 90, 70, 100, p, sync=True).endswith(" checked")
+        assert gpu.describe_plan(3, 90, 70, 100, p, sync=True).split(" est=")[0].endswith(" checked")
         seqs, offs = gpu.pack_batch(triples)
         assert np.array_equal(gpu.score_batch(triples, p), orc.score_batch(seqs, offs, op, nthreads=3))
 
@@ -720,7 +720,7 @@ def test_literal_helix_matches_oracle(gpu, orc, monkeypatch, bits, s3_mode):
             h = rng.integers(0, 4, L).astype(np.uint8)
             triples.append((h, h[: int(rng.integers(1, L + 1))].copy(), h[: int(rng.integers(1, L + 1))].copy()))
         ml = [max(len(t[k]) for t in triples) for k in range(3)]
-        assert gpu.describe_plan(len(triples), *ml, p, kernel="plane") == "plane literal-helix"
+        assert gpu.describe_plan(len(triples), *ml, p, kernel="plane").startswith("plane literal-helix")
         seqs, offs = gpu.pack_batch(triples)
         ws = gpu.workspace_size(len(triples), *ml, p, "plane")
         import torch
@@ -825,3 +825,32 @@ def test_literal_lap_1024_rtl_words(gpu, orc, synth):
     s, fin = gpu.score(a, b, c, p, kernel="plane", final_states=True)
     assert (s, tuple(fin)) == orc.score(a, b, c, op, final_states=True)
     assert gpu.fallback_count() == before
+
+
+@pytest.mark.parametrize("kernel,mode", [("pencil", "lap"), ("plane", "litlap")])
+def test_lap_chunked_batch(gpu, orc, monkeypatch, kernel, mode):
+    """A batch run as several lap launches of a few triples each, one after
+    another on the stream (lap_geom_chunked; TSA_LAP_CHUNK forces 3): the
+    last, smaller chunk on its own geometry inside the batch's workspace,
+    the factored and the literal form, async path -- every score the oracle's."""
+    import torch
+    monkeypatch.setenv("TSA_PENCIL_MODE", mode)
+    monkeypatch.setenv("TSA_LAP_CHUNK", "3")
+    rng = np.random.default_rng(91 if kernel == "pencil" else 92)
+    triples = [tuple(rng.integers(0, 5, int(rng.integers(lo, hi))).astype(np.uint8) for lo, hi in
+                     ((40, 150), (17, 45), (65, 140))) for _ in range(8)]
+    p, op = gpu.TsaParams.default(score_bits=12), orc.default_params(score_bits=12)
+    ml = [max(len(t[k]) for t in triples) for k in range(3)]
+    plan = gpu.describe_plan(len(triples), *ml, p, kernel=kernel, sync=False)
+    assert " lap" in plan and "literal-lap" in plan if kernel == "plane" else " lap " in plan
+    assert "chunk=3" in plan, plan
+    seqs, offs = gpu.pack_batch(triples)
+    ws = gpu.workspace_size(len(triples), *ml, p, kernel)
+    d_seqs, d_offs = torch.from_numpy(seqs).cuda(), torch.from_numpy(offs).cuda()
+    d_sc = torch.full((len(triples),), -7, dtype=torch.int32, device="cuda")
+    d_ws = torch.zeros(max(ws, 16), dtype=torch.uint8, device="cuda")
+    for _ in range(2):  # a second pass over the same workspace: new epochs, stale rings ignored
+        gpu.score_batch_async(d_seqs.data_ptr(), d_offs.data_ptr(), len(triples), *ml, d_sc.data_ptr(),
+                              d_ws.data_ptr(), ws, torch.cuda.current_stream().cuda_stream, p, kernel)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_sc.cpu().numpy(), orc.score_batch(seqs, offs, op, nthreads=8)), plan
