@@ -86,6 +86,11 @@ struct LapPart {
 // error word d_err (cleared by the caller) are on the last part's device.
 int lap_launch_split(const LapGeom &g, bool f16, bool sop, const PencilArgs &pa, const LapPart *parts,
                      int np, int32_t *d_score, uint32_t *d_err);
+// The same in the literal arithmetic (lap_kernel LIT, any parameter set), on a
+// geometry from literal_split_geom.
+int lap_launch_split_lit(const LapGeom &g, bool sop, const KParams &kp, const LapPart *parts, int np,
+                         int32_t *d_score, uint32_t *d_err);
+LapGeom literal_split_geom(int32_t la, int32_t lb, int32_t lc, bool sop, int np);
 // The lap geometry of one (la, lb, lc) cube for an np-way split (.ok = false
 // when the factored form has no lap schedule for it or fewer than np laps),
 // and its launch (arithmetic chosen as pencil_launch_batch would).

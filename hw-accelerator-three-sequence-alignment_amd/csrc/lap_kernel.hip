@@ -445,7 +445,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   static_assert(!(CHK && F16), "the checked kernel runs the int16 form");
   static_assert(!(CHK && SYS), "a split cube runs the unchecked forms");
-  static_assert(!(LIT && (F16 || CHK || SYS)), "the literal form: int16, unchecked, one device");
+  static_assert(!(LIT && (F16 || CHK)), "the literal form: int16, unchecked");
   constexpr int SCOPE = SYS ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
   constexpr int RW = 2 * NW, ZT = 64 * M, LPD = lap_pd(M), K = lap_k(M), K0 = lap_k0(M);
   constexpr int PAIR = 64 * REC_BYTES, SLOT = M * PAIR;
@@ -1610,10 +1610,8 @@ int lap_launch(const LapGeom &g, bool f16, bool sop, const uint8_t *d_seqs,
 // part p+1's workspace and part p+1's first lap copies its progress words into
 // part p's, so each hand-off crossing the link is a posted store and every
 // poll stays local. The error word and the score live with the last part.
-template <int M, int NW, bool F16, bool SOP>
-static int launch_lap_split(const LapGeom &g, const PencilArgs &pa, const LapPart *parts, int np,
-                            int32_t *d_score, uint32_t *d_err) {
-  auto kfn = lap_kernel<M, NW, F16, SOP, false, true>;
+static int launch_split_fn(LapKernelFn kfn, int NW, const LapGeom &g, const PencilArgs &pa, const LitArgs &lit,
+                           const LapPart *parts, int np, int32_t *d_score, uint32_t *d_err) {
   const uint32_t epoch = lap_next_epoch();
   const uint32_t spin = lap_spin_limit();
   for (int p = 0; p < np; ++p) {
@@ -1632,19 +1630,42 @@ static int launch_lap_split(const LapGeom &g, const PencilArgs &pa, const LapPar
                        q.d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, lap_rounds(g, q.d_ws), prog,
                        d_err, d_score,
                        (int32_t *)nullptr, pa, epoch, spin, q.L0, q.L1, yf_out, prog_in,
-                       (unsigned long long *)nullptr, LitArgs{});
+                       (unsigned long long *)nullptr, lit);
     if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
   }
   return TSA_OK;
 }
+template <int M, int NW, bool F16, bool SOP>
+static int launch_lap_split(const LapGeom &g, const PencilArgs &pa, const LapPart *parts, int np,
+                            int32_t *d_score, uint32_t *d_err) {
+  return launch_split_fn(lap_kernel<M, NW, F16, SOP, false, true>, NW, g, pa, LitArgs{}, parts, np, d_score, d_err);
+}
+template <int M, int NW, bool SOP>
+static int launch_lap_split_lit(const LapGeom &g, const PencilArgs &pa, const LitArgs &lit, const LapPart *parts,
+                                int np, int32_t *d_score, uint32_t *d_err) {
+  return launch_split_fn(lap_kernel<M, NW, false, SOP, false, true, true>, NW, g, pa, lit, parts, np, d_score,
+                         d_err);
+}
+static int split_parts_ok(const LapGeom &g, const LapPart *parts, int np) {
+  if (np < 1 || g.lds > LDS_MAX) return 0;
+  for (int p = 0; p < np; ++p)
+    if (parts[p].L0 >= parts[p].L1 || parts[p].L0 != (p ? parts[p - 1].L1 : 0)) return 0;
+  return parts[np - 1].L1 == g.G;
+}
 
 int lap_launch_split(const LapGeom &g, bool f16, bool sop, const PencilArgs &pa, const LapPart *parts,
                      int np, int32_t *d_score, uint32_t *d_err) {
-  if (np < 1 || g.lds > LDS_MAX) return TSA_EINVAL;
-  for (int p = 0; p < np; ++p)
-    if (parts[p].L0 >= parts[p].L1 || parts[p].L0 != (p ? parts[p - 1].L1 : 0)) return TSA_EINVAL;
-  if (parts[np - 1].L1 != g.G) return TSA_EINVAL;
+  if (!split_parts_ok(g, parts, np)) return TSA_EINVAL;
   return TSA_LAP_SHAPES(launch_lap_split, g.M, g.NW, f16, sop, g, pa, parts, np, d_score, d_err);
+}
+
+int lap_launch_split_lit(const LapGeom &g, bool sop, const KParams &kp, const LapPart *parts, int np,
+                         int32_t *d_score, uint32_t *d_err) {
+  if (!split_parts_ok(g, parts, np) || g.M > 2 || (g.NW != 4 && g.NW != 8)) return TSA_EINVAL;
+  PencilArgs pa{};  // as lap_launch_lit: the packed flag only, zero faces
+  pa.packed = kp.packed;
+  const LitArgs lit = lit_args(kp);
+  return TSA_LIT_SHAPES(launch_lap_split_lit, g.M, g.NW, sop, g, pa, lit, parts, np, d_score, d_err);
 }
 
 }  // namespace tsa

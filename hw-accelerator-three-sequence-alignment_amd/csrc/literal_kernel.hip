@@ -92,6 +92,17 @@ static LapGeom literal_lap_choice(int32_t n, int32_t max_la, int32_t max_lb, int
     }
   return best;
 }
+// One cube split over np devices by laps in the literal arithmetic: the
+// literal lap's geometry with full-length rings (pencil_split_geom's reasons),
+// if it has at least np laps.
+LapGeom literal_split_geom(int32_t la, int32_t lb, int32_t lc, bool sop, int np) {
+  LapGeom g = literal_lap_choice(1, la, lb, lc, sop, LAP_RESIDENT);
+  if (np < 1 || !g.ok || g.G < np) {
+    g.ok = false;
+    return g;
+  }
+  return lap_geom(1, la, lb, lc, g.M, g.NW, true, false, sop, true);
+}
 int literal_kind(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, bool sop, int lap) {
   const bool helix_ok = literal_shape_ok(max_la, max_lb, max_lc);
   if (const char *e = getenv("TSA_PENCIL_MODE")) {  // test knobs

@@ -484,11 +484,13 @@ int tsa_score_gpu_multi(const uint8_t *a, int32_t la, const uint8_t *b, int32_t 
   if (nd <= 0) return TSA_ENODEV;
   for (int32_t i = 0; i < n_devices; ++i)
     if (devices[i] < 0 || devices[i] >= nd) return TSA_ENODEV;
-  if (!pencil_exact(p, la, lb, lc)) return TSA_ERANGE;  // the factored form, exact a priori
+  // the factored form where it is exact a priori, else the literal arithmetic
+  const bool exact = pencil_exact(p, la, lb, lc);
   KParams kp;
   if ((rc = build_kparams(p, &kp))) return rc;
   const Range bound = value_bound(p, la, lb, lc);
-  const LapGeom g = pencil_split_geom(la, lb, lc, kp, bound, n_devices);
+  const LapGeom g = exact ? pencil_split_geom(la, lb, lc, kp, bound, n_devices)
+                          : literal_split_geom(la, lb, lc, p->s3_mode == TSA_S3_SOP, n_devices);
   if (!g.ok) return TSA_ERANGE;  // no lap schedule, or fewer laps than parts
   const int np = n_devices;
   const size_t ws_bytes = lap_workspace_bytes(g);
@@ -563,7 +565,8 @@ int tsa_score_gpu_multi(const uint8_t *a, int32_t la, const uint8_t *b, int32_t 
   }
   t0 = now_us();
   launched = true;
-  rc = pencil_launch_split(g, kp, bound, parts.data(), np, d_score, d_err);
+  rc = exact ? pencil_launch_split(g, kp, bound, parts.data(), np, d_score, d_err)
+             : lap_launch_split_lit(g, p->s3_mode == TSA_S3_SOP, kp, parts.data(), np, d_score, d_err);
   if (rc) goto done;
   for (int i = 0; i < np; ++i) {
     HIPCHK(hipSetDevice(parts[i].device));

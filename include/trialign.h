@@ -168,12 +168,13 @@ int tsa_pack2(const uint8_t *syms, int64_t n, uint8_t *out);
  * n_devices contiguous runs, part i on devices[i]; the last lap of part i
  * hands its y records to part i+1 by system-scope stores into part i+1's
  * fine-grained workspace over xGMI (peer access is enabled between the listed
- * devices). A device may be listed more than once: its parts then run as
- * concurrent launches on separate streams of that device. Requires the
- * factored form to be exact a priori (else TSA_ERANGE) and at least n_devices
- * laps (TSA_ERANGE). A timed-out hand-off returns TSA_EINTERNAL (never a
- * silent score). wall_us (nullable): host wall time from the first launch to
- * the last part's completion. */
+ * devices). A device may be listed more than once: its parts then run one
+ * after another on one stream of that device. The factored arithmetic where
+ * it is exact a priori, else the RTL's literal wrapped arithmetic (any
+ * parameter set); TSA_ERANGE with fewer laps than n_devices (or no lap
+ * schedule). A timed-out hand-off returns TSA_EINTERNAL (never a silent
+ * score). wall_us (nullable): host wall time from the first launch to the last
+ * part's completion. */
 int tsa_score_gpu_multi(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
                         const uint8_t *c, int32_t lc, const tsa_params *p,
                         const int32_t *devices, int32_t n_devices, int32_t *score,

@@ -653,8 +653,8 @@ def test_split_cube_int16_and_ragged(gpu, orc, synth):
 
 
 def test_split_cube_errors(gpu, synth):
-    """Fewer laps than parts, bad device ids and a non-exact parameter set are
-    refused with the reference-style error codes, never a silent score."""
+    """Fewer laps than parts and bad device ids are refused with the
+    reference-style error codes, never a silent score."""
     a, b, c = synth.triple(1, 16)
     with pytest.raises(gpu.TsaError) as e:
         gpu.score_multi(a, b, c, [0] * 8)   # 16 rows = 2 laps < 8 parts
@@ -662,12 +662,32 @@ def test_split_cube_errors(gpu, synth):
     with pytest.raises(gpu.TsaError) as e:
         gpu.score_multi(a, b, c, [gpu.device_count()])
     assert e.value.rc == gpu.TSA_ENODEV
-    # the a-priori bound of a 1024^3 cube leaves the RTL's 12-bit word: the
-    # split (factored form, exact a priori only) refuses it
-    a, b, c = synth.triple(1, 1024)
-    with pytest.raises(gpu.TsaError) as e:
-        gpu.score_multi(a, b, c, [0, 0], gpu.TsaParams.default(score_bits=12))
-    assert e.value.rc == gpu.TSA_ERANGE
+
+
+@pytest.mark.parametrize("kw", [dict(score_bits=6), dict(gap_open=1, gap_extend=2, score_bits=12),
+                                dict(score_bits=9, s3_mode=1)])
+def test_split_cube_literal(gpu, orc, synth, kw):
+    """Parameter sets the factored form cannot run exactly split in the
+    literal arithmetic (lap_kernel LIT with system-scope hand-offs): narrow
+    words that wrap, GO < GE, SOP s3 -- 2 and 3 parts, ragged, equal to the
+    oracle's literal score."""
+    p, op = gpu.TsaParams.default(**kw), orc.default_params(**kw)
+    rng = np.random.default_rng(55)
+    h = rng.integers(0, 4, 170).astype(np.uint8)
+    cases = [synth.triple(5, 150), (h, h[:133].copy(), h[:149].copy())]
+    for a, b, c in cases:
+        ref = orc.score(a, b, c, op)
+        for parts in ([0, 0], [0, 0, 0]):
+            assert gpu.score_multi(a, b, c, parts, p)[0] == ref, (kw, parts, len(b))
+
+
+def test_split_cube_literal_1024_rtl_words(gpu, orc, synth):
+    """configs[3]'s 1024^3 cube with the RTL's 12-bit words (beyond the
+    factored form's a-priori bound) split in 2 parts in the literal
+    arithmetic: the oracle's literal score."""
+    a, b, c = synth.triple(0, 1024)
+    p = gpu.TsaParams.default(score_bits=12)
+    assert gpu.score_multi(a, b, c, [0, 0], p)[0] == orc.score(a, b, c, orc.default_params(score_bits=12))
 
 
 def test_split_cube_timeout_is_reported_not_silent(gpu, synth, monkeypatch):
