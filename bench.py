@@ -483,8 +483,8 @@ def start_single_oracles(args, synth, L):
         log("oracle unavailable:", e)
         return None
     want = sorted({(Ls, bits) for _, Ls, bits, _, _ in single_specs(args, L)}, key=lambda t: -t[0])
-    if not args.no_extra_configs:  # the split child process times 256^3 (12-bit) and 1024^3 (16-bit)
-        want = sorted(set(want) | {(256, 12), (1024, 16)}, key=lambda t: -t[0])
+    if not args.no_extra_configs:  # the split child process times 256^3 (12-bit), 1024^3 (16- and 12-bit)
+        want = sorted(set(want) | {(256, 12), (1024, 16), (1024, 12)}, key=lambda t: -t[0])
     pool = ThreadPoolExecutor(max_workers=max(1, min(len(want), host_cores())))
     futs = {(Ls, bits): pool.submit(lambda Ls=Ls, bits=bits: oracle.score(
         *synth.triple(0, Ls), oracle.default_params(score_bits=bits))) for Ls, bits in want}
@@ -530,7 +530,7 @@ def oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single, pending)
         sp = single.get("split over devices")
         errors = {}
         if isinstance(sp, dict):
-            lens = [k for k in sp if k.endswith("^3")]
+            lens = [k for k in sp if "^3" in k and isinstance(sp[k], dict)]
             devs = sp.get("devices")
             if isinstance(devs, str):  # the child failed before printing ("0,1")
                 devs = [int(d) for d in devs.split(",") if d.strip().isdigit()]
@@ -544,7 +544,7 @@ def oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single, pending)
                 else:
                     put("split over devices", None, None)
             for k in lens:
-                Ls = int(k[:-2])
+                Ls = int(k.split("^3")[0])
                 for part in ("one_part", "split"):
                     r = sp[k].get(part, {})
                     name = f"split over devices {devs}: {k} {part}"

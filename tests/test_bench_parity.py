@@ -56,3 +56,7 @@ def test_parity_leg_counts_configs_and_split(tsa, orc, synth):
     assert parity["mismatches"] == 0 and parity["errors"] == {"split over devices": "rc=1: boom"}
     parity, _ = _leg(tsa, orc, synth, {"devices": "0,0", "error": "rc=1: boom"})
     assert parity["mismatches"] == 1
+    # a labelled length (the literal 12-bit case) is checked like the others
+    parity, _ = _leg(tsa, orc, synth, {"devices": [0, 0], "16^3 (12-bit RTL words, literal)": {
+        "score_bits": 12, "one_part": ok(s0), "split": ok(s0)}})
+    assert parity["mismatches"] == 0 and len([k for k in parity["configs"] if "literal" in k]) == 2

@@ -33,16 +33,19 @@ def load_pkg():
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--devices", default="0,0")
-    ap.add_argument("--lengths", default="256,1024")
+    # "1024r": 1024^3 with the RTL's 12-bit words -- beyond the factored form's
+    # a-priori bound, so the split runs the literal arithmetic
+    ap.add_argument("--lengths", default="256,1024,1024r")
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args(argv)
     tsa = load_pkg()
     import tsa_amd.synth as synth  # noqa: E402
     devs = [int(d) for d in args.devices.split(",")]
     out = {"devices": devs, "timing": "host wall: first launch .. last part synchronised, median"}
-    for L in (int(v) for v in args.lengths.split(",")):
+    for spec in args.lengths.split(","):
+        L, rtl = int(spec.rstrip("r")), spec.endswith("r")
         # 16-bit words beyond the RTL's envelope (as bench's configs[3] line)
-        prm = tsa.TsaParams.default(score_bits=12 if L <= 512 else 16)
+        prm = tsa.TsaParams.default(score_bits=12 if (L <= 512 or rtl) else 16)
         a, b, c = synth.triple(0, L)
         rec = {"score_bits": prm.score_bits}
         for label, dl in (("one_part", devs[:1]), ("split", devs)):
@@ -61,7 +64,7 @@ def main(argv=None):
             if rec[label]["score"] is None:
                 rec[label]["error"] = f"repetitions disagree: {sorted(scores)}"
         rec["same_score"] = rec["one_part"].get("score") == rec["split"].get("score") is not None
-        out[f"{L}^3"] = rec
+        out[f"{L}^3" + (" (12-bit RTL words, literal)" if rtl else "")] = rec
     print(json.dumps(out))
 
 
