@@ -57,6 +57,8 @@ BYTES_PER_CELL = 28            # 7 int16 states written + read onc
 VALU_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 4
 VALU_PEAK_SOURCE = ("profiles/r3_valu_peak.jsonl (tools/valu_peak.hip: packed-16 ops 0.24 "
                     "instr/cycle/SIMD; 2-cycle control v_add_u32 0.43; MI355X_MICROARCH.md:54,473)")
+# Cubes the split-over-devices leg times (tools/split_cube.py --lengths)
+SPLIT_LENGTHS = "256,1024"
 # Paper Table III (pic/Result.png): ASIC runtime per N^3 cube, ms
 ASIC_MS = {64: 0.03, 128: 0.19, 256: 1.39, 512: 10.82}
 
@@ -457,7 +459,8 @@ def time_split(world_devices: int) -> dict:
     process with its own time limit: 2 parts sharing device 0 at N = 1,
     devices 0..N-1 on an N-GPU run (rank 0, while the other ranks wait)."""
     devs = ",".join(str(d) for d in range(world_devices)) if world_devices > 1 else "0,0"
-    cmd = [sys.executable, os.path.join(ROOT, "tools", "split_cube.py"), "--devices", devs]
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "split_cube.py"), "--devices", devs,
+           "--lengths", SPLIT_LENGTHS]
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=180)
         if r.returncode == 0 and r.stdout.strip():
