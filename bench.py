@@ -58,7 +58,7 @@ VALU_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 4
 VALU_PEAK_SOURCE = ("profiles/r3_valu_peak.jsonl (tools/valu_peak.hip: packed-16 ops 0.24 "
                     "instr/cycle/SIMD; 2-cycle control v_add_u32 0.43; MI355X_MICROARCH.md:54,473)")
 # Cubes the split-over-devices leg times (tools/split_cube.py --lengths)
-SPLIT_LENGTHS = "256,1024"
+SPLIT_LENGTHS = "256,1024,1024r"  # 1024r: the RTL's 12-bit words, literal split
 # Paper Table III (pic/Result.png): ASIC runtime per N^3 cube, ms
 ASIC_MS = {64: 0.03, 128: 0.19, 256: 1.39, 512: 10.82}
 
