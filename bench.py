@@ -67,7 +67,12 @@ ASIC_MS = {64: 0.03, 128: 0.19, 256: 1.39, 512: 10.82}
 KERNEL_SOURCES = {
     "pencil_kernel": ["pencil_kernel.hip", "pencil_kernel.h", "pencil_common.h", "tsa_internal.h"],
     "plane_step_kernel": ["plane_kernel.hip", "tsa_internal.h"],
+    "lap_kernel": ["lap_kernel.hip", "lap_kernel.h", "pencil_common.h", "pencil_kernel.h", "tsa_internal.h"],
 }
+# Lane-operations per cell of the V-space pair core (cell_messages_vs: 24
+# packed instructions per pair of cells = 12 per cell), the algorithmic VALU
+# work of one cell; DESIGN.md 4.2
+CORE_LANE_OPS_PER_CELL = 12
 
 
 def log(*a):
@@ -157,6 +162,82 @@ def spawn_ranks(n: int, argv: list[str], script: str = __file__) -> int:
     return (abs(bad[0]) or 1) if bad else 0
 
 
+PROFILE_WARMUP, PROFILE_STEPS, PROFILE_SINGLE_REPS = 3, 10, 9
+
+
+def run_profile_child(args) -> dict:
+    """rocprofv3 --kernel-trace --stats over this same bench (the program
+    directly after --): a child process that runs PROFILE_WARMUP + PROFILE_STEPS
+    batch launches and PROFILE_SINGLE_REPS + 1 single configs[2] cubes on the
+    same box, before this process touches the GPU. Returns the stats rows of
+    the batch kernel and the single-cube lap kernel ({} with an "error" when
+    the profiler is absent or fails) and the csv path, so the line's
+    roofline.frac comes from the profiled average of this run's own box."""
+    import csv
+    import shutil
+    import signal
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return {"error": "rocprofv3 not found"}
+    out = os.path.abspath(args.profile_dir or os.path.join(ROOT, "gpurun_out", "bench_profile"))
+    os.makedirs(out, exist_ok=True)
+    cmd = [prof, "--kernel-trace", "--stats", "-d", out, "-o", "run", "--output-format", "csv", "--",
+           sys.executable, os.path.abspath(__file__), "--profile-child", "--steps", str(PROFILE_STEPS),
+           "--warmup", str(PROFILE_WARMUP), "--per-gpu", str(args.per_gpu), "--length", str(args.length),
+           "--score-bits", str(args.score_bits), "--kernel", args.kernel, "--workload", args.workload]
+    env = dict(os.environ, TMPDIR="/tmp")
+    t0 = time.perf_counter()
+    try:
+        p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                             text=True, start_new_session=True)
+        try:
+            _, err = p.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.communicate()
+            return {"error": "rocprofv3 child timed out (300 s)"}
+        if p.returncode != 0:
+            return {"error": f"rocprofv3 child rc={p.returncode}: {err.strip()[-300:]}"}
+        stats = os.path.join(out, "run_kernel_stats.csv")
+        with open(stats) as f:
+            rows = list(csv.DictReader(f))
+    except Exception as e:  # noqa: BLE001  (recorded: the line falls back to the live time)
+        return {"error": str(e)[-300:]}
+    res = {"csv": os.path.relpath(stats, ROOT) if stats.startswith(ROOT) else stats,
+           "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --profile-child "
+                      f"--steps {PROFILE_STEPS} --warmup {PROFILE_WARMUP}",
+           "child_s": round(time.perf_counter() - t0, 1)}
+    for r in rows:
+        name = r["Name"]
+        for key in ("pencil_kernel", "lap_kernel", "plane_step_kernel", "literal_kernel"):
+            if f"tsa::{key}<" in name and key not in res:
+                res[key] = {"name": name.split("(")[0], "calls": int(r["Calls"]),
+                            "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
+                            "max_ns": float(r["MaxNs"])}
+    return res
+
+
+def profile_child_main(args) -> int:
+    """The program rocprofv3 traces (run_profile_child): the batch hot path,
+    warmup + steps launches, then the configs[2] single cube; no output line."""
+    import torch
+    torch.cuda.set_device(0)
+    tsa = load_pkg()
+    import tsa_amd.synth as synth  # noqa: E402
+    L = args.length
+    n = args.per_gpu if args.workload == "batch" else 1
+    params = tsa.TsaParams.default(score_bits=args.score_bits)
+    seqs, offs = synth.batch(0, n, L)
+    hot = GpuBatch(tsa, torch.device("cuda", 0), seqs, offs - offs[0], n, L, params, args.kernel)
+    for _ in range(args.warmup + args.steps):
+        hot.step()
+    hot.sync()
+    args.no_extra_configs = True
+    time_singles(args, tsa, synth, hot, torch.device("cuda", 0), L, params, reps=PROFILE_SINGLE_REPS)
+    hot.sync()
+    return 0
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -175,6 +256,11 @@ def parse_args(argv=None):
                     help="batch triples checked vs the oracle (both ends included); 0 = no parity leg")
     ap.add_argument("--score-bits", type=int, default=12,
                     help="12 = RTL wrap (default); 16/0 for cubes beyond the RTL envelope (1024^3)")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="skip the rocprofv3 kernel-trace child (roofline.frac from the live time only)")
+    ap.add_argument("--profile-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--profile-dir", default=None,
+                    help="where the rocprofv3 child writes (default gpurun_out/bench_profile)")
     return ap.parse_args(argv)
 
 
@@ -218,7 +304,7 @@ class GpuBatch:
 
 
 def run_rank(args, world: int, rank: int, local_rank: int, backend: str, make_batch,
-             device=None, extras: bool = True, on_scores=None):
+             device=None, extras: bool = True, on_scores=None, prof=None):
     """One rank of the bench: shard, stage, warm up, time K steps between
     barriers, take the max over ranks, gather the scores (the one collective)
     and, on rank 0, return the JSON record. make_batch(tsa, dev, seqs, offs, n,
@@ -273,6 +359,15 @@ def run_rank(args, world: int, rank: int, local_rank: int, backend: str, make_ba
     kernel_ms_per_step = hot.elapsed_ms(ev0, ev1) / args.steps
     elapsed_max = shard.max_over_ranks(elapsed, dev)
 
+    # what this rank saw: the collective's world (RCCL under "nccl") and the
+    # devices visible to it, so an N-GPU line shows RCCL ran N ranks
+    devices = {"backend": (backend if world > 1 else "none (single process)"),
+               "dist_world_size": dist.get_world_size() if world > 1 else 1,
+               "visible_devices": torch.cuda.device_count() if backend == "nccl" else 0,
+               "device": str(dev)}
+    if backend == "nccl":
+        devices["device_name"] = torch.cuda.get_device_name(dev)
+
     cells_per_triple = L * L * L
     total_cells = n_total * cells_per_triple * args.steps
     gcups = total_cells / elapsed_max / 1e9
@@ -284,7 +379,8 @@ def run_rank(args, world: int, rank: int, local_rank: int, backend: str, make_ba
     rec = None
     if rank == 0:
         rec = report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gcups,
-                     ms_per_step, kernel_ms_per_step, all_scores, extras)
+                     ms_per_step, kernel_ms_per_step, all_scores, extras, prof)
+        rec["config"]["devices"] = devices
         if on_scores is not None:  # test hook: the gathered scores, global order
             on_scores(rec, all_scores)
     if world > 1:
@@ -294,7 +390,8 @@ def run_rank(args, world: int, rank: int, local_rank: int, backend: str, make_ba
 
 
 def report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gcups, ms_per_step,
-           kernel_ms_per_step, all_scores, extras):
+           kernel_ms_per_step, all_scores, extras, prof=None):
+    prof = prof or {}
     kind = args.kernel
     if kind == "auto":  # AUTO = pencil whenever its factored arithmetic is exact
         kind = "pencil" if _pencil_ok(tsa, L, params) else "plane"
@@ -324,20 +421,36 @@ def report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gc
                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(algo_gbs / HBM_PEAK_GBS, 4),
                  "note": "SURVEY.md 8d: 7 int16 states written + read once per cell; the pencil "
                          "kernel keeps states in registers/LDS, so this model is not its ceiling"}
+    kprof = prof.get(kernel_name)
     if insts and kind == "pencil":
-        # the binding resource of the pencil kernel: VALU issue
-        ach = insts / kernel_s
+        # the binding resource of the pencil kernel: VALU issue. frac: the
+        # rocprofv3 average of this run's own profiled child (same box, same
+        # command); frac_live: the live HIP-event time of the timed steps
+        live = insts / kernel_s
+        prof_s = kprof["avg_ns"] * 1e-9 if kprof else None
+        ach = insts / prof_s if prof_s else live
         roofline = {"bound": "valu", "achieved": round(ach / 1e9, 2),
                     "peak": VALU_WAVE_INSTR_PER_S / 1e9, "unit": "G wave-instr/s",
-                    "frac": round(ach / VALU_WAVE_INSTR_PER_S, 4), "traffic": traffic,
+                    "frac": round(ach / VALU_WAVE_INSTR_PER_S, 4),
+                    "frac_live": round(live / VALU_WAVE_INSTR_PER_S, 4),
+                    "achieved_live": round(live / 1e9, 2), "traffic": traffic,
                     "peak_source": VALU_PEAK_SOURCE, "insts_per_launch": insts,
                     "lane_insts_per_cell": round(insts * 64 / per_gpu_cells, 3),
-                    "source": f"SQ_INSTS_VALU per launch (profiles/pmc_{kernel_name}_"
-                              f"{args.workload}.json) / live kernel time (HIP events)"}
+                    # the V-space pair core's 12 lane-ops per cell at the line's rate:
+                    # how far the cells/s are from what the issue ceiling allows
+                    "algorithmic": round(gcups / world * 1e9 * CORE_LANE_OPS_PER_CELL / 64
+                                         / VALU_WAVE_INSTR_PER_S, 4),
+                    "algorithmic_note": f"value/n_gpus x {CORE_LANE_OPS_PER_CELL} lane-ops per cell "
+                                        "(cell_messages_vs pair core) / (64 x peak)",
+                    "source": (f"SQ_INSTS_VALU per launch (profiles/pmc_{kernel_name}_{args.workload}.json)"
+                               " / " + ("rocprofv3 average of the profiled child (profile)" if prof_s
+                                        else "live kernel time (HIP events; no profile: "
+                                        + str(prof.get("error", "skipped")) + ")"))}
     else:  # no current profile: the contract's HBM form on algorithmic bytes
         roofline = dict(hbm_model, traffic=traffic)
     roofline.update({"kernel": kernel_name, "kernel_ms_per_step": round(kernel_ms_per_step, 4),
-                     "hbm": hbm, "hbm_model": hbm_model, "pmc_stale": pmc.get("stale")})
+                     "hbm": hbm, "hbm_model": hbm_model, "pmc_stale": pmc.get("stale"),
+                     "profile": prof or None})
 
     # the single cubes' oracle scores (two 1024^3 among them, ~30 s each on
     # one core) run in threads while the GPU times the cubes
@@ -345,6 +458,7 @@ def report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gc
     single = {}
     if extras:
         single = time_singles(args, tsa, synth, hot, dev, L, params)
+        roofline["single_cube_lap"] = lap_roofline(args, L, single, prof)
     parity, cpu_baseline = None, None
     if extras and args.check > 0:
         parity, cpu_baseline = oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single,
@@ -381,6 +495,29 @@ def report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gc
     }
 
 
+def lap_roofline(args, L, single, prof) -> dict | None:
+    """VALU roofline of the single-cube lap kernel on configs[2] (one L^3
+    cube): SQ_INSTS_VALU per launch from the stamped committed PMC profile
+    (profiles/pmc_lap_kernel_single.json) over the profiled child's average
+    (frac) and the live median (frac_live). The lap kernel is latency-bound
+    (DESIGN.md 4.4): this says how much of the chip's issue it uses."""
+    r = single.get(f"configs[2]: {L}^3", {})
+    if "ms" not in r:
+        return None
+    pmc = load_pmc("lap_kernel", "single")
+    insts = pmc.get("valu_insts_per_launch") if L == 256 else None
+    kp = (prof or {}).get("lap_kernel")
+    out = {"bound": "valu", "kernel": "lap_kernel", "cube": f"{L}^3", "plan": r.get("plan"),
+           "peak": VALU_WAVE_INSTR_PER_S / 1e9, "unit": "G wave-instr/s", "ms_live": r["ms"],
+           "insts_per_launch": insts, "pmc_stale": pmc.get("stale")}
+    if insts:
+        out["frac_live"] = round(insts / (r["ms"] * 1e-3) / VALU_WAVE_INSTR_PER_S, 4)
+        if kp:
+            out["profiled_avg_ms"] = round(kp["avg_ns"] * 1e-6, 4)
+            out["frac"] = round(insts / (kp["avg_ns"] * 1e-9) / VALU_WAVE_INSTR_PER_S, 4)
+    return out
+
+
 def single_specs(args, L):
     """(key, length, score_bits, reps, kernel) of every single cube rank 0
     times: configs[2] (L^3, the batch's words), configs[1] (64^3), the
@@ -402,40 +539,65 @@ def single_specs(args, L):
     return specs
 
 
-def time_singles(args, tsa, synth, hot, dev, L, params):
-    """Single-cube latency (single_specs): median of individually timed calls
-    on the launch stream. Each cube is synth.triple(0, length)."""
+DAT_KEY = "configs[0]: dat/{A,B,C}_seq.dat"
+
+
+def dat_triple():
+    """The reference's dat/{A,B,C}_seq.dat triple, as committed numbers
+    (tests/golden/golden.json case "dat", golden score 1)."""
+    with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+        return next(c for c in json.load(f)["cases"] if c["name"] == "dat")
+
+
+def time_singles(args, tsa, synth, hot, dev, L, params, reps=None):
+    """Single-cube latency (single_specs, plus the dat triple): median of
+    individually timed calls on the launch stream. Each cube is
+    synth.triple(0, length)."""
     import torch
     stream = hot.stream
 
-    def one(Ls, prm, reps, kernel=None):
+    def one(Ls, prm, nrep, kernel=None, trip=None):
         kernel = kernel or args.kernel
-        sa = synth.batch(0, 1, Ls)
+        sa = synth.batch(0, 1, Ls) if trip is None else tsa.pack_batch([trip])
+        la, lb, lc = (int(sa[1][i + 1] - sa[1][i]) for i in range(3))
         s_seqs = torch.from_numpy(sa[0]).to(dev)
         s_offs = torch.from_numpy(sa[1]).to(dev)
         s_score = torch.zeros(1, dtype=torch.int32, device=dev)
-        s_ws = tsa.workspace_size(1, Ls, Ls, Ls, prm, kernel)
+        s_ws = tsa.workspace_size(1, la, lb, lc, prm, kernel)
         s_wsb = torch.empty(max(s_ws, 16), dtype=torch.uint8, device=dev)
 
         def sstep():
-            tsa.score_batch_async(s_seqs.data_ptr(), s_offs.data_ptr(), 1, Ls, Ls, Ls,
+            tsa.score_batch_async(s_seqs.data_ptr(), s_offs.data_ptr(), 1, la, lb, lc,
                                   s_score.data_ptr(), s_wsb.data_ptr(), s_ws, stream.cuda_stream,
                                   prm, kernel)
         sstep()
         torch.cuda.synchronize()
-        times = []
-        for _ in range(reps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            sstep()
-            e1.record(stream)
-            torch.cuda.synchronize()
-            times.append(e0.elapsed_time(e1))
-        sms = float(np.median(times))
-        r = {"ms": round(sms, 4), "gcups": round(Ls ** 3 / (sms * 1e-3) / 1e9, 3),
+
+        def timed(preload):
+            # preload: the batch launch queued first keeps the GPU busy while
+            # the host submits e0, the cube's launch(es) and e1, so e0 -> e1 is
+            # the device time of the call; without it the span also holds the
+            # host's submission latency (the round-3 figure)
+            times = []
+            for _ in range(reps or nrep):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                if preload:
+                    hot.step()
+                e0.record(stream)
+                sstep()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                times.append(e0.elapsed_time(e1))
+            return float(np.median(times))
+        sms = timed(preload=hot.n > 0)
+        r = {"ms": round(sms, 4), "gcups": round(la * lb * lc / (sms * 1e-3) / 1e9, 3),
              "score": int(s_score.item()), "score_bits": prm.score_bits,
-             "plan": tsa.describe_plan(1, Ls, Ls, Ls, prm, kernel=kernel, sync=False)}
-        if Ls in ASIC_MS and prm.score_bits == 12:
+             "plan": tsa.describe_plan(1, la, lb, lc, prm, kernel=kernel, sync=False),
+             "timing": "device: median of HIP events around the call's launches, queued behind a "
+                       "batch launch so host submission is hidden" if hot.n > 0 else "events, host submit included"}
+        if hot.n > 0:
+            r["ms_incl_submit"] = round(timed(preload=False), 4)
+        if Ls in ASIC_MS and prm.score_bits == 12 and trip is None:
             r["asic_ms"] = ASIC_MS[Ls]
             r["vs_asic"] = round(ASIC_MS[Ls] / sms, 3)
         if kernel == "checked":
@@ -443,13 +605,19 @@ def time_singles(args, tsa, synth, hot, dev, L, params):
         return r
 
     out = {}
-    for key, Ls, bits, reps, kernel in single_specs(args, L):
+    for key, Ls, bits, nrep, kernel in single_specs(args, L):
         try:
-            out[key] = one(Ls, tsa.TsaParams.default(score_bits=bits), reps, kernel)
+            out[key] = one(Ls, tsa.TsaParams.default(score_bits=bits), nrep, kernel)
         except Exception as e:  # noqa: BLE001  (recorded; the parity leg counts it)
             log(f"single-cube {key} failed:", e)
             out[key] = {"error": str(e)[-300:], "score_bits": bits}
     if not args.no_extra_configs:
+        dat = dat_triple()
+        try:  # the testbench's own input on the device-resident path (AUTO kernel)
+            out[DAT_KEY] = one(64, tsa.TsaParams.default(), 15, "auto", (dat["a"], dat["b"], dat["c"]))
+        except Exception as e:  # noqa: BLE001
+            log("dat triple failed:", e)
+            out[DAT_KEY] = {"error": str(e)[-300:], "score_bits": 12}
         out["split over devices"] = time_split(world_devices=args.gpus)
     return out
 
@@ -476,10 +644,22 @@ def _import_oracle():
     return oracle
 
 
+CPU_REPS_SMALL, CPU_REPS_LARGE = 5, 1  # oracle repetitions per single cube: <= 512^3 / 1024^3
+
+
 def start_single_oracles(args, synth, L):
-    """Oracle scores of every single cube bench times (and splits), keyed by
-    (length, score_bits), started in threads (the C oracle releases the GIL)."""
+    """Oracle scores of every single cube bench times (and splits) and of the
+    dat triple, keyed by (length, score_bits) / "dat", started in threads (the
+    C oracle releases the GIL) that overlap the GPU timings. Each is also the
+    software baseline of its config, as the reference's Table III "software"
+    row (pic/Result.png): one core, the median of CPU_REPS_SMALL runs up to
+    512^3 and one run at 1024^3. The threads are pinned one per core to the
+    LAST cores of the job's affinity set and capped below the core count, so
+    the launching thread keeps a core of its own (timed launches of small
+    cubes are not inflated by them). Future -> (score, [seconds per run])."""
     from concurrent.futures import ThreadPoolExecutor
+    import itertools
+    import threading
     try:
         oracle = _import_oracle()
     except Exception as e:  # noqa: BLE001
@@ -488,9 +668,37 @@ def start_single_oracles(args, synth, L):
     want = sorted({(Ls, bits) for _, Ls, bits, _, _ in single_specs(args, L)}, key=lambda t: -t[0])
     if not args.no_extra_configs:  # the split child process times 256^3 (12-bit), 1024^3 (16- and 12-bit)
         want = sorted(set(want) | {(256, 12), (1024, 16), (1024, 12)}, key=lambda t: -t[0])
-    pool = ThreadPoolExecutor(max_workers=max(1, min(len(want), host_cores())))
-    futs = {(Ls, bits): pool.submit(lambda Ls=Ls, bits=bits: oracle.score(
-        *synth.triple(0, Ls), oracle.default_params(score_bits=bits))) for Ls, bits in want}
+    try:
+        allowed = sorted(os.sched_getaffinity(0))[: host_cores()]
+    except AttributeError:
+        allowed = list(range(host_cores()))
+    nthr = max(1, min(len(want) + 1, len(allowed) - 2))
+    cores = allowed[-nthr:]
+    counter = itertools.count()
+
+    def pin():
+        try:
+            os.sched_setaffinity(0, {cores[next(counter) % len(cores)]})  # this thread only (Linux)
+        except (AttributeError, OSError):
+            pass
+
+    def run(a, b, c, prm, reps):
+        times, score = [], None
+        for _ in range(reps):
+            t = oracle.now()
+            score = oracle.score(a, b, c, prm)
+            times.append(oracle.now() - t)
+        return score, times
+
+    pool = ThreadPoolExecutor(max_workers=nthr, initializer=pin)
+    futs = {(Ls, bits): pool.submit(run, *synth.triple(0, Ls), oracle.default_params(score_bits=bits),
+                                    CPU_REPS_LARGE if Ls > 512 else CPU_REPS_SMALL)
+            for Ls, bits in want}
+    if not args.no_extra_configs:
+        dat = dat_triple()
+        futs["dat"] = pool.submit(run, dat["a"], dat["b"], dat["c"], oracle.default_params(), CPU_REPS_SMALL)
+    futs["_pinning"] = {"threads": nthr, "cores": cores, "of": len(allowed),
+                        "main_thread": threading.current_thread().name}
     pool.shutdown(wait=False)
     return futs
 
@@ -525,11 +733,27 @@ def oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single, pending)
         bad = [int(i) for i, g, r in zip(idx, got, ref) if g != r]
         batch = {"checked": len(idx), "indices": [int(i) for i in idx], "mismatches": len(bad),
                  "mismatched_indices": bad, "score_bits": args.score_bits}
-        # single cubes and the split (oracle scores started before the GPU timings)
-        refs = {k: f.result() for k, f in pending.items()} if pending else {}
+        # single cubes and the split (oracle scores started before the GPU timings);
+        # each one's 1-core oracle time is the config's software baseline
+        pin_info = pending.pop("_pinning", None) if pending else None
+        done = {k: f.result() for k, f in pending.items()} if pending else {}
+        refs = {k: v[0] for k, v in done.items()}
+        cpu_ms = {k: round(float(np.median(v[1])) * 1e3, 3) for k, v in done.items()}
+
+        def baseline(r, key):
+            if key in cpu_ms and isinstance(r, dict):
+                r["cpu_ms"] = cpu_ms[key]
+                r["cpu_runs"] = len(done[key][1])
+                if r.get("ms"):
+                    r["speedup"] = round(cpu_ms[key] / r["ms"], 2)
+
         for key, Ls, bits, _, _ in single_specs(args, L):
             r = single.get(key, {})
             put(key, r.get("score"), refs.get((Ls, bits)))
+            baseline(r, (Ls, bits))
+        if DAT_KEY in single:
+            put(DAT_KEY + " (device-resident path)", single[DAT_KEY].get("score"), refs.get("dat"))
+            baseline(single[DAT_KEY], "dat")
         sp = single.get("split over devices")
         errors = {}
         if isinstance(sp, dict):
@@ -548,13 +772,24 @@ def oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single, pending)
                     put("split over devices", None, None)
             for k in lens:
                 Ls = int(k.split("^3")[0])
+                okey = (Ls, sp[k]["score_bits"])
+                if okey in cpu_ms:
+                    sp[k]["cpu_ms"] = cpu_ms[okey]
                 for part in ("one_part", "split"):
                     r = sp[k].get(part, {})
                     name = f"split over devices {devs}: {k} {part}"
-                    if cross and part == "split" and r.get("score") is None:
+                    # only a setup failure of the cross-device split (no peer
+                    # access, no such device: TSA_EDEVICE / TSA_ENODEV) is
+                    # non-failing; repetitions that disagree, a timed-out hand-off
+                    # or a wrong score fail the parity leg
+                    if (cross and part == "split" and r.get("score") is None and not r.get("disagree")
+                            and r.get("rc") in (-3, -4)):
                         errors[name] = r.get("error", "no score")
                         continue
-                    put(name, r.get("score"), refs.get((Ls, sp[k]["score_bits"])))
+                    put(name, r.get("score"), refs.get(okey))
+                    if r.get("disagree"):
+                        configs[name]["ok"] = False
+                        configs[name]["disagree"] = r.get("scores")
         # the reference's own parity input: dat/{A,B,C}_seq.dat through tsa_score_gpu
         with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
             dat = next(c for c in json.load(f)["cases"] if c["name"] == "dat")
@@ -571,6 +806,8 @@ def oracle_leg(args, tsa, synth, world, n_total, L, all_scores, single, pending)
         n_bad = len(bad) + sum(not c["ok"] for c in configs.values())
         parity = {"mismatches": n_bad, "batch": batch, "configs": configs,
                   "against": "oracle/tsa_oracle.c (literal RTL form, same inputs)"}
+        if pin_info:
+            parity["oracle_threads"] = dict(pin_info, overlapped="the single-cube GPU timings")
         if errors:
             parity["errors"] = errors
         if world == 1 and not args.no_cpu_baseline:
@@ -618,7 +855,16 @@ def main(argv=None):
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    rec = run_rank(args, world, rank, local_rank, "nccl", GpuBatch)
+    if args.profile_child:
+        sys.exit(profile_child_main(args))
+    prof = None
+    if world == 1 and not args.no_profile:
+        # before this process touches the GPU: the same workload under
+        # rocprofv3 on this box, for the line's profiled roofline
+        prof = run_profile_child(args)
+        if prof.get("error"):
+            log("profile child:", prof["error"])
+    rec = run_rank(args, world, rank, local_rank, "nccl", GpuBatch, prof=prof)
     if rec is not None:
         print(json.dumps(rec), flush=True)
         par = rec.get("parity")

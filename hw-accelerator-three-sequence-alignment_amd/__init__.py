@@ -63,7 +63,7 @@ EXPORTS = (
     "tsa_score_batch", "tsa_batch_workspace_size", "tsa_score_batch_async",
     "tsa_device_count", "tsa_strerror", "tsa_version", "tsa_describe_plan", "tsa_align_gpu",
     "tsa_fallback_count", "tsa_check_fallback_count", "tsa_score_batch_async_p2", "tsa_pack2",
-    "tsa_score_gpu_multi",
+    "tsa_score_gpu_multi", "tsa_score_batch_devices",
 )
 
 # Score of a triple the device could not score (include/trialign.h).
@@ -127,6 +127,8 @@ def _load_lib() -> ctypes.CDLL:
                                      ctypes.c_int32, pp, ctypes.c_int32, i32p, i32p,
                                      ctypes.c_int32]
     lib.tsa_score_batch.argtypes = [u8p, i64p, ctypes.c_int32, pp, i32p, ctypes.c_int32]
+    lib.tsa_score_batch_devices.argtypes = [u8p, i64p, ctypes.c_int32, pp, i32p, i32p,
+                                            ctypes.c_int32]
     lib.tsa_batch_workspace_size.argtypes = [ctypes.c_int32] * 4 + [pp, ctypes.c_int32,
                                                                    ctypes.POINTER(ctypes.c_size_t)]
     lib.tsa_score_batch_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
@@ -154,7 +156,7 @@ def _load_lib() -> ctypes.CDLL:
     for name in ("tsa_validate", "tsa_score_gpu", "tsa_score_gpu_ex", "tsa_score_batch",
                  "tsa_batch_workspace_size", "tsa_score_batch_async", "tsa_device_count",
                  "tsa_describe_plan", "tsa_align_gpu", "tsa_score_batch_async_p2", "tsa_pack2",
-                 "tsa_score_gpu_multi"):
+                 "tsa_score_gpu_multi", "tsa_score_batch_devices"):
         getattr(lib, name).restype = ctypes.c_int
     return lib
 
@@ -260,7 +262,7 @@ def score_multi(a, b, c, devices: Sequence[int], params: Optional[TsaParams] = N
     """One triple's cube split over several GPUs by laps (tsa_score_gpu_multi):
     ``(score, wall_us)``. The reference's pencil slicing with face SRAMs
     between pencils (src/TriAlign_1cyc.v:78-98,127-140) spread over devices;
-    a device listed twice runs two concurrent parts on one GPU."""
+    a device listed twice runs its parts one after another on one GPU."""
     p = params or TsaParams.default()
     A, B, C = _as_u8(a), _as_u8(b), _as_u8(c)
     devs = np.ascontiguousarray(np.asarray(list(devices), dtype=np.int32))
@@ -385,6 +387,27 @@ def score_batch(triples=None, params: Optional[TsaParams] = None, n_devices: int
     rc = _lib.tsa_score_batch(_ptr(seqs, ctypes.c_uint8), _ptr(offsets, ctypes.c_int64), n,
                               ctypes.byref(p), _ptr(out, ctypes.c_int32), n_devices)
     _check(rc, "tsa_score_batch")
+    return out[:n]
+
+
+def score_batch_devices(triples=None, devices: Sequence[int] = (0,),
+                        params: Optional[TsaParams] = None, seqs: Optional[np.ndarray] = None,
+                        offsets: Optional[np.ndarray] = None) -> np.ndarray:
+    """tsa_score_batch_devices: contiguous shards of the batch, shard s on
+    ``devices[s]``; a device may repeat ((0, 0, 0) shards three ways on one
+    GPU, its shards run one after another)."""
+    p = params or TsaParams.default()
+    if seqs is None:
+        seqs, offsets = pack_batch(triples)
+    seqs = np.ascontiguousarray(seqs, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    devs = np.ascontiguousarray(np.asarray(list(devices), dtype=np.int32))
+    n = (len(offsets) - 1) // 3
+    out = np.zeros(max(n, 1), dtype=np.int32)
+    rc = _lib.tsa_score_batch_devices(_ptr(seqs, ctypes.c_uint8), _ptr(offsets, ctypes.c_int64), n,
+                                      ctypes.byref(p), _ptr(out, ctypes.c_int32),
+                                      _ptr(devs, ctypes.c_int32), len(devs))
+    _check(rc, "tsa_score_batch_devices")
     return out[:n]
 
 

@@ -1274,11 +1274,19 @@ static DevInfo dev_info() {
 // occupancy API counts waves per CU instead and reads one workgroup high at
 // the SGPR edge (MI355X_MICROARCH.md:463) and, measured, at 96 VGPRs with
 // 9-wave workgroups (it said 2, the CU ran 1).
+// The bound is taken over every instantiation of the shape and form -- the
+// checked (CHK) and split (SYS) ones too, whose register counts can differ
+// from the plain kernel's -- so the grid plan holds whichever of them runs.
 int lap_simd_blocks_per_cu(int M, int NW, bool f16, bool sop, bool lit) {
-  char prefix[80];  // lap_kernel<M, NW, F16, SOP, CHK = 0, SYS = 0, LIT>
-  snprintf(prefix, sizeof prefix, "_ZN3tsa10lap_kernelILi%dELi%dELb%dELb%dELb0ELb0ELb%dE", M, NW, f16 ? 1 : 0,
-           sop ? 1 : 0, lit ? 1 : 0);
-  const int sgpr = kernel_sgpr_max(prefix), vgpr = kernel_vgpr_max(prefix);
+  int sgpr = -1, vgpr = -1;
+  for (int chk = 0; chk < 2; ++chk)
+    for (int sys = 0; sys < 2; ++sys) {
+      char prefix[80];  // lap_kernel<M, NW, F16, SOP, CHK, SYS, LIT>
+      snprintf(prefix, sizeof prefix, "_ZN3tsa10lap_kernelILi%dELi%dELb%dELb%dELb%dELb%dELb%dE", M, NW,
+               f16 ? 1 : 0, sop ? 1 : 0, chk, sys, lit ? 1 : 0);
+      sgpr = std::max(sgpr, kernel_sgpr_max(prefix));
+      vgpr = std::max(vgpr, kernel_vgpr_max(prefix));
+    }
   const int waves = std::min(sgpr_waves_per_simd(sgpr < 0 ? 112 : sgpr), vgpr_waves_per_simd(vgpr < 0 ? 256 : vgpr));
   return waves / ((NW + 1 + 3) / 4);
 }

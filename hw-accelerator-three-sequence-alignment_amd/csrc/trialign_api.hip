@@ -446,10 +446,12 @@ int tsa_score_gpu(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb, co
   return tsa_score_gpu_ex(a, la, b, lb, c, lc, p, TSA_KERNEL_AUTO, score, nullptr, device);
 }
 
-int tsa_score_batch(const uint8_t *seqs, const int64_t *offsets, int32_t n, const tsa_params *p,
-                    int32_t *scores, int32_t n_devices) {
-  if (!seqs || !offsets || !scores || n < 0 || !params_ok(p)) return TSA_EINVAL;
-  if (n == 0) return TSA_OK;
+int tsa_score_batch_devices(const uint8_t *seqs, const int64_t *offsets, int32_t n,
+                            const tsa_params *p, int32_t *scores, const int32_t *devices,
+                            int32_t n_devices) {
+  if (!seqs || !offsets || !scores || !devices || n < 0 || n_devices < 1 || n_devices > 1024 ||
+      !params_ok(p))
+    return TSA_EINVAL;
   for (int32_t i = 0; i < n; ++i) {
     const int64_t *o = offsets + 3 * (int64_t)i;
     if (o[1] < o[0] || o[2] < o[1] || o[3] < o[2]) return TSA_EINVAL;
@@ -457,20 +459,57 @@ int tsa_score_batch(const uint8_t *seqs, const int64_t *offsets, int32_t n, cons
                           seqs + o[2], (int32_t)(o[3] - o[2]), p);
     if (rc) return rc;
   }
+  if (n == 0) return TSA_OK;
   const int nd = tsa_device_count();
   if (nd <= 0) return TSA_ENODEV;
-  const int use = std::max(1, std::min(n_devices <= 0 ? nd : n_devices, std::min(nd, n)));
-  std::vector<int> rcs(use, TSA_OK);
+  for (int32_t i = 0; i < n_devices; ++i)
+    if (devices[i] < 0 || devices[i] >= nd) return TSA_ENODEV;
+  // shard s = contiguous triples [n s / ns, n (s+1) / ns) on devices[s]; one
+  // host thread per DISTINCT device runs that device's shards in list order
+  // (shards sharing a device never run concurrently: a lap grid's residency
+  // plan assumes it has the device to itself)
+  const int ns = std::min<int32_t>(n_devices, n);
+  std::vector<int> dev_of_thread;
+  std::vector<std::vector<int>> shards_of_thread;
+  for (int s = 0; s < ns; ++s) {
+    const int d = devices[s];
+    size_t k = 0;
+    while (k < dev_of_thread.size() && dev_of_thread[k] != d) ++k;
+    if (k == dev_of_thread.size()) {
+      dev_of_thread.push_back(d);
+      shards_of_thread.emplace_back();
+    }
+    shards_of_thread[k].push_back(s);
+  }
+  std::vector<int> rcs(ns, TSA_OK);
   std::vector<std::thread> th;
-  for (int d = 0; d < use; ++d) {
-    const int32_t i0 = (int32_t)((int64_t)n * d / use), i1 = (int32_t)((int64_t)n * (d + 1) / use);
-    th.emplace_back([&, d, i0, i1] {
-      rcs[d] = run_host_batch_on_device(d, seqs, offsets, i0, i1, p, TSA_KERNEL_AUTO, scores, nullptr);
+  for (size_t k = 0; k < dev_of_thread.size(); ++k) {
+    th.emplace_back([&, k] {
+      for (int s : shards_of_thread[k]) {
+        const int32_t i0 = (int32_t)((int64_t)n * s / ns), i1 = (int32_t)((int64_t)n * (s + 1) / ns);
+        rcs[s] = run_host_batch_on_device(dev_of_thread[k], seqs, offsets, i0, i1, p, TSA_KERNEL_AUTO,
+                                          scores, nullptr);
+        if (rcs[s]) break;
+      }
     });
   }
   for (auto &t : th) t.join();
   for (int r : rcs) if (r) return r;
   return TSA_OK;
+}
+
+int tsa_score_batch(const uint8_t *seqs, const int64_t *offsets, int32_t n, const tsa_params *p,
+                    int32_t *scores, int32_t n_devices) {
+  if (!seqs || !offsets || !scores || n < 0 || !params_ok(p)) return TSA_EINVAL;
+  const int nd = tsa_device_count();
+  if (nd <= 0) {  // validation, then TSA_ENODEV (TSA_OK for n == 0)
+    const int32_t d0 = 0;
+    return tsa_score_batch_devices(seqs, offsets, n, p, scores, &d0, 1);
+  }
+  const int use = std::max(1, std::min(n_devices <= 0 ? nd : n_devices, std::max(1, std::min(nd, n))));
+  std::vector<int32_t> devs((size_t)use);
+  for (int d = 0; d < use; ++d) devs[d] = d;
+  return tsa_score_batch_devices(seqs, offsets, n, p, scores, devs.data(), use);
 }
 
 int tsa_score_gpu_multi(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,

@@ -129,15 +129,30 @@ int tsa_score_gpu_ex(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb,
 int tsa_score_batch(const uint8_t *seqs, const int64_t *offsets, int32_t n,
                     const tsa_params *p, int32_t *scores, int32_t n_devices);
 
+/* tsa_score_batch over an explicit device list: the batch is cut into
+ * min(n_devices, n) contiguous shards, shard s (triples [n*s/ns, n*(s+1)/ns))
+ * on devices[s]. A device may be listed more than once ({0,0,0} shards a
+ * batch three ways on one GPU): one host thread per distinct device runs its
+ * shards one after another. Same replacement of the testbench's one-shot
+ * caller (src/TriAlign_tb.sv:279-333) as tsa_score_batch, which is this call
+ * with devices {0..n_devices-1}. TSA_ENODEV for a device index out of range. */
+int tsa_score_batch_devices(const uint8_t *seqs, const int64_t *offsets, int32_t n,
+                            const tsa_params *p, int32_t *scores,
+                            const int32_t *devices, int32_t n_devices);
+
 /* Device-resident batch. d_seqs/d_offsets/d_scores are device pointers on the
  * current device; stream is a hipStream_t (NULL = default stream). The
  * workspace must hold tsa_batch_workspace_size() bytes. max_l* bound every
  * triple's lengths. Launches only; no host synchronisation. Validation of
  * symbols is the caller's job on this path (tsa_validate on the host copy).
- * For a few large cubes this path may run the single-cube (lap) kernel, whose
- * workgroups hand data to each other; it only does so when the whole grid is
- * co-resident, and if a hand-off still times out the affected triples read
- * TSA_SCORE_INVALID once the stream has synchronised -- check for it. */
+ * For a few large cubes this path may run the single-cube (lap) schedule --
+ * the factored lap kernel, or for TSA_KERNEL_PLANE the literal lap kernel --
+ * whose workgroups hand data to each other. Its grid may span several
+ * dispatch rounds (up to three, one workgroup per CU); that relies on the
+ * in-order per-XCD workgroup dispatch measured on MI355X, which HIP does not
+ * promise. Every hand-off wait is bounded: if one times out, the affected
+ * triples read TSA_SCORE_INVALID once the stream has synchronised -- check
+ * for it on every kernel choice, TSA_KERNEL_PLANE included. */
 int tsa_batch_workspace_size(int32_t n, int32_t max_la, int32_t max_lb,
                              int32_t max_lc, const tsa_params *p,
                              int32_t kernel, size_t *bytes);

@@ -191,6 +191,24 @@ def test_no_cpu_fallback_without_gpu(tsa):
     with pytest.raises(tsa.TsaError) as e:
         tsa.score_multi([0] * 64, [0] * 64, [0] * 64, [0, 1])
     assert e.value.rc == tsa.TSA_ENODEV
+    with pytest.raises(tsa.TsaError) as e:
+        tsa.score_batch_devices([([0], [1], [2])], (0, 0))
+    assert e.value.rc == tsa.TSA_ENODEV
+    # an empty batch is not an error, with or without a device
+    assert len(tsa.score_batch_devices([], (0,))) == 0
+
+
+def test_batch_devices_argument_checks(tsa):
+    """tsa_score_batch_devices validates before touching a device: an empty
+    device list, a bad symbol or bad offsets are TSA_EINVAL on any host."""
+    for devs, trip in [((), [([0], [1], [2])]), ((0, 0), [([0, 9], [1], [2])])]:
+        with pytest.raises(tsa.TsaError) as e:
+            tsa.score_batch_devices(trip, devs)
+        assert e.value.rc == tsa.TSA_EINVAL, devs
+    seqs = np.zeros(6, np.uint8)
+    with pytest.raises(tsa.TsaError) as e:  # offsets not monotone
+        tsa.score_batch_devices(devices=(0,), seqs=seqs, offsets=np.array([0, 3, 2, 6], np.int64))
+    assert e.value.rc == tsa.TSA_EINVAL
 
 
 def test_cli_reports_no_device_or_score():

@@ -33,7 +33,8 @@ def _leg(tsa, orc, synth, split):
     args = Namespace(check=3, score_bits=12, no_extra_configs=True, no_cpu_baseline=True, cpu_seconds=1)
     single = {f"configs[2]: {L}^3": {"score": ref[0]}, "split over devices": split}
     scores = np.array([ref[i] for i in range(n)], dtype=np.int32)
-    parity, _ = bench.oracle_leg(args, GpuStandIn, synth, 1, n, L, scores, single, {(L, 12): _done(ref[0])})
+    pending = {(L, 12): _done((ref[0], [0.002, 0.001, 0.003])), "_pinning": {"threads": 1, "cores": [0]}}
+    parity, _ = bench.oracle_leg(args, GpuStandIn, synth, 1, n, L, scores, single, pending)
     return parity, ref[0]
 
 
@@ -50,8 +51,21 @@ def test_parity_leg_counts_configs_and_split(tsa, orc, synth):
     parity, _ = _leg(tsa, orc, synth, {"devices": [0, 1], "16^3": {"score_bits": 12, "one_part": ok(s0), "split": ok(s0 + 1)}})
     assert parity["mismatches"] == 1
     parity, _ = _leg(tsa, orc, synth, {"devices": [0, 1], "16^3": {"score_bits": 12, "one_part": ok(s0),
-                                                                  "split": {"parts": 2, "error": "peer access"}}})
+                                                                  "split": {"parts": 2, "error": "peer access",
+                                                                            "rc": -4}}})
     assert parity["mismatches"] == 0 and list(parity["errors"].values()) == ["peer access"]
+    # ... but only a setup failure: a timed-out hand-off (TSA_EINTERNAL) fails
+    parity, _ = _leg(tsa, orc, synth, {"devices": [0, 1], "16^3": {"score_bits": 12, "one_part": ok(s0),
+                                                                  "split": {"parts": 2, "error": "timeout",
+                                                                            "rc": -6}}})
+    assert parity["mismatches"] == 1 and "errors" not in parity
+    # repetitions that disagree always fail, on one GPU and across GPUs
+    dis = {"parts": 2, "us": 1.0, "score": None, "disagree": True, "scores": [s0, s0 + 1],
+           "error": "repetitions disagree"}
+    for devs in ([0, 1], [0, 0]):
+        parity, _ = _leg(tsa, orc, synth, {"devices": devs, "16^3": {"score_bits": 12, "one_part": ok(s0),
+                                                                    "split": dis}})
+        assert parity["mismatches"] == 1 and "errors" not in parity, devs
     parity, _ = _leg(tsa, orc, synth, {"devices": "0,1", "error": "rc=1: boom"})
     assert parity["mismatches"] == 0 and parity["errors"] == {"split over devices": "rc=1: boom"}
     parity, _ = _leg(tsa, orc, synth, {"devices": "0,0", "error": "rc=1: boom"})
@@ -60,3 +74,28 @@ def test_parity_leg_counts_configs_and_split(tsa, orc, synth):
     parity, _ = _leg(tsa, orc, synth, {"devices": [0, 0], "16^3 (12-bit RTL words, literal)": {
         "score_bits": 12, "one_part": ok(s0), "split": ok(s0)}})
     assert parity["mismatches"] == 0 and len([k for k in parity["configs"] if "literal" in k]) == 2
+
+
+def test_single_cube_software_baseline(tsa, orc, synth):
+    """Every timed single cube carries the 1-core oracle time of the same
+    input (median of its runs) and the speedup over it, as the reference's
+    Table III "software" row does."""
+    import bench
+    L, n = 16, 4
+    ref = orc.score(*synth.triple(0, L))
+    single = {f"configs[2]: {L}^3": {"score": ref, "ms": 0.5}}
+    args = Namespace(check=2, score_bits=12, no_extra_configs=True, no_cpu_baseline=True, cpu_seconds=1)
+    pending = {(L, 12): _done((ref, [0.002, 0.004, 0.003]))}
+    scores = np.array([orc.score(*synth.triple(i, L)) for i in range(n)], dtype=np.int32)
+
+    class GpuStandIn:
+        pack_batch = staticmethod(tsa.pack_batch)
+
+        @staticmethod
+        def score(a, b, c, device=0):
+            return orc.score(a, b, c)
+
+    parity, _ = bench.oracle_leg(args, GpuStandIn, synth, 1, n, L, scores, single, pending)
+    assert parity["mismatches"] == 0
+    r = single[f"configs[2]: {L}^3"]
+    assert r["cpu_ms"] == 3.0 and r["speedup"] == 6.0 and r["cpu_runs"] == 3

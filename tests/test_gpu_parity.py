@@ -128,6 +128,31 @@ def test_ragged_batch(gpu, orc):
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("devices", [(0, 0, 0), (0, 0), (0,) * 7])
+def test_batch_devices_repeated(gpu, orc, devices):
+    """tsa_score_batch_devices with a repeated device list: the host path that
+    shards a batch over devices (one thread per distinct device, shards split,
+    scores gathered in place) runs on one GPU. Ragged lengths so shards plan
+    different kernels (helix, two-triple helix, lap)."""
+    rng = np.random.default_rng(len(devices))
+    triples = []
+    for i in range(23):
+        hi = 300 if i % 5 == 0 else 70
+        la, lb, lc = (int(v) for v in rng.integers(1, hi, 3))
+        triples.append(tuple(rng.integers(0, 5, n).astype(np.uint8) for n in (la, lb, lc)))
+    got = gpu.score_batch_devices(triples, devices)
+    seqs, offs = gpu.pack_batch(triples)
+    assert np.array_equal(got, orc.score_batch(seqs, offs, nthreads=8))
+    # more shards than triples: each triple its own shard
+    two = triples[:2]
+    s2, o2 = gpu.pack_batch(two)
+    assert np.array_equal(gpu.score_batch_devices(two, devices), orc.score_batch(s2, o2))
+    # error paths: a device out of range refuses before any work
+    with pytest.raises(gpu.TsaError) as e:
+        gpu.score_batch_devices(triples, (0, gpu.device_count()))
+    assert e.value.rc == gpu.TSA_ENODEV
+
+
 def test_related_high_scores(gpu, orc, synth):
     for seed in range(3):
         a, b, c = synth.related_triple(seed, 200)

@@ -63,9 +63,10 @@ def sgpr_waves(sgpr):
 @pytest.mark.parametrize("NW", [4, 8])
 def test_lap_residency_sgpr_cap(tsa, meta, M, NW):
     """lap_simd_blocks_per_cu(M, NW, f16, sop, lit) = the SGPR / VGPR waves per
-    SIMD over the waves a workgroup may put on one SIMD, from the table's
-    single-device instantiation (CHK = SYS = 0) of that form; the literal form
-    (LIT, int16, M <= 2) has its own."""
+    SIMD over the waves a workgroup may put on one SIMD, taken over EVERY
+    instantiation of that shape and form -- single-device, checked (CHK) and
+    split (SYS) -- so the plan holds whichever of them launches; the literal
+    form (LIT, int16, M <= 2) has its own."""
     fn = getattr(tsa.lib(), "_ZN3tsa22lap_simd_blocks_per_cuEiibbb")
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_bool, ctypes.c_bool, ctypes.c_bool]
@@ -73,12 +74,19 @@ def test_lap_residency_sgpr_cap(tsa, meta, M, NW):
     if M <= 2:
         forms += [(False, sop, True) for sop in (False, True)]
     for f16, sop, lit in forms:
-        pre = f"_ZN3tsa10lap_kernelILi{M}ELi{NW}ELb{int(f16)}ELb{int(sop)}ELb0ELb0ELb{int(lit)}E"
-        sg = max(v["sgpr"] for k, v in meta.items() if k.startswith(pre))
-        vg = max(v["vgpr"] + v.get("agpr", 0) for k, v in meta.items() if k.startswith(pre))
+        pres = [f"_ZN3tsa10lap_kernelILi{M}ELi{NW}ELb{int(f16)}ELb{int(sop)}ELb{chk}ELb{sys}ELb{int(lit)}E"
+                for chk in (0, 1) for sys in (0, 1)]
+        rows = [v for k, v in meta.items() if any(k.startswith(p) for p in pres)]
+        sg = max(v["sgpr"] for v in rows)
+        vg = max(v["vgpr"] + v.get("agpr", 0) for v in rows)
         want = min(sgpr_waves(sg), vgpr_waves(vg)) // ((NW + 1 + 3) // 4)
         assert fn(M, NW, f16, sop, lit) == want, (f16, sop, lit)
         assert want >= 1
+        # no instantiation of the form (checked / split included) admits fewer
+        # workgroups per CU than the bound the plan uses
+        for v in rows:
+            own = min(sgpr_waves(v["sgpr"]), vgpr_waves(v["vgpr"] + v.get("agpr", 0))) // ((NW + 1 + 3) // 4)
+            assert own >= want
     if M <= 2:  # the literal form keeps its registers in registers
         lit = [k for k in meta if re.match(rf"_ZN3tsa10lap_kernelILi{M}ELi{NW}ELb0ELb[01]ELb0ELb0ELb1EE", k)]
         assert len(lit) == 2 and all(meta[k].get("scratch", 0) == 0 for k in lit)

@@ -82,6 +82,17 @@ def main(tag="r1"):
                     ent["valu_insts"] = statistics.mean(pmc[key]["SQ_INSTS_VALU"])
             ks[f"{kname}@{grid}"] = ent
         summary[kdir] = ks
+        # bench.py's single-cube lap roofline: the lap launch of the profiled
+        # child's configs[2] cube (one lap instantiation runs there)
+        laps = [v for v in ks.values() if "lap_kernel" in v["kernel"] and v.get("valu_insts")]
+        if laps:
+            lp = max(laps, key=lambda v: v["dispatches"])
+            with open(os.path.join(outdir, "pmc_lap_kernel_single.json"), "w") as f:
+                json.dump({"tag": tag, "kernel": lp["kernel"], "grid_size": lp["grid_size"],
+                           "avg_ns": lp["avg_ns"], "hbm_bytes_per_launch": lp.get("hbm_bytes_corrected"),
+                           "valu_insts_per_launch": lp["valu_insts"],
+                           "kernel_source_sha256": kernel_source_hash("lap_kernel"),
+                           "workload": "bench.py --profile-child: configs[2], one 256^3 cube"}, f, indent=1)
         # bench.py traffic: the batch launch = the largest grid of the main kernel
         main_k = [v for v in ks.values() if ("pencil_kernel" in v["kernel"] or "plane_step_kernel" in v["kernel"])]
         if main_k:

@@ -56,12 +56,17 @@ def main(argv=None):
                     scores.add(s)
                     walls.append(w)
             except Exception as e:  # noqa: BLE001  (recorded: no score, bench counts it)
-                rec[label] = {"parts": len(dl), "error": str(e)[-300:]}
+                # rc: TSA_EDEVICE / TSA_ENODEV are setup failures (peer access, no
+                # such device); anything else is a failure of the split itself
+                rec[label] = {"parts": len(dl), "error": str(e)[-300:], "rc": getattr(e, "rc", None)}
                 continue
-            # every repetition must agree (a differing one reads as no score)
+            # every repetition must agree: a differing one is flagged "disagree",
+            # which bench.py's parity leg always counts as a failure
             rec[label] = {"parts": len(dl), "us": round(float(np.median(walls[1:])), 1),
                           "score": scores.pop() if len(scores) == 1 else None}
             if rec[label]["score"] is None:
+                rec[label]["disagree"] = True
+                rec[label]["scores"] = sorted(scores)
                 rec[label]["error"] = f"repetitions disagree: {sorted(scores)}"
         rec["same_score"] = rec["one_part"].get("score") == rec["split"].get("score") is not None
         out[f"{L}^3" + (" (12-bit RTL words, literal)" if rtl else "")] = rec
