@@ -24,7 +24,8 @@ struct LapGeom {
   int32_t YR, ZR;    // slim y / z ring slots per workgroup (powers of 2)
   int32_t SX, KBY, KBZ, YRB, ZRB;  // rounds: slots per XCD, boundary rings (LapRounds)
   int32_t per_cu;    // workgroups a CU holds (per-SIMD register model, occupancy API)
-  int64_t blocks;    // grid (padding blocks for the XCD-aware tile mapping)
+  int64_t blocks;    // logical workgroups (padding blocks for the XCD-aware tile mapping)
+  int64_t grid;      // physical grid: one dispatch round (8 SX), each block looping over its rounds
   size_t lds, prog_bytes, yf_bytes, zf_bytes, yb_bytes, zb_bytes;
   int64_t waves;     // dispatch rounds: 1 = every workgroup resident at once
   double est_us;     // estimated latency (lap_geom_chunked: of every launch)
@@ -35,9 +36,11 @@ struct LapGeom {
   int32_t max_la, max_lb, max_lc;
 };
 
-// A grid beyond the resident slots runs in dispatch rounds (boundary rings
-// keep a producer from waiting on a later round); limited to a few.
-constexpr int64_t LAP_MAX_WAVES = 3;
+// A grid beyond the resident slots runs in rounds: the launch holds one
+// round, every workgroup looping over its slots' later rounds in lap order
+// (boundary rings keep a producer from waiting on a later round); limited to
+// a few (the boundary rings grow with them).
+constexpr int64_t LAP_MAX_WAVES = 4;
 
 // Geometry of the lap schedule (M pairs per lane, NW waves) for a batch of n
 // triples; full_rings: every ring as long as the cube (no back-pressure: the
@@ -46,8 +49,7 @@ constexpr int64_t LAP_MAX_WAVES = 3;
 LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW,
                  bool full_rings, bool f16, bool sop, bool lit = false);
 // A batch of n triples as sequential launches of `chunk` triples each, so
-// that every launch's grid keeps to the dispatch-round rules (at most
-// LAP_MAX_WAVES rounds, one workgroup per CU when there are several): the
+// that every launch's grid keeps to at most LAP_MAX_WAVES rounds: the
 // chunk of least total estimated latency (TSA_LAP_CHUNK forces one, tests).
 // .ok = false when no chunk size fits.
 LapGeom lap_geom_chunked(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW, bool f16,

@@ -55,6 +55,7 @@
 
 #include <atomic>
 #include <ctime>
+#include <mutex>
 #include <vector>
 
 #include "pencil_common.h"
@@ -396,10 +397,10 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 // a 1024^3 lap grid started only as the first half finished (ring-lag census,
 // profiles/r3e_lap_lag.jsonl). M = 1 fits 6 as it is; M >= 4 runs one per CU.
 #ifndef TSA_LAP_WPE2
-#define TSA_LAP_WPE2 5
+#define TSA_LAP_WPE2 4
 #endif
 __host__ __device__ constexpr int lap_waves_per_eu(int M, bool lit = false) {
-  return lit ? (M == 1 ? 4 : 3) : M == 1 ? 4 : M == 2 ? TSA_LAP_WPE2 : 2;
+  return lit ? (M == 1 ? 6 : 3) : M == 1 ? 6 : M == 2 ? TSA_LAP_WPE2 : 2;
 }
 // f(integral_constant<J>) for J = B .. E-1, unrolled at compile time
 template <int B, int E, class F>
@@ -433,15 +434,39 @@ __device__ __forceinline__ void static_for(F &&f) {
 // step) into the rings wave 0 and position 0 read, values are shifted left by
 // 16 - SCORE_BITS so int16 adds wrap at the RTL word, and the final cell's 7
 // input states go to mon (aux) as its final 7-tuple.
+// The kernel's arguments, one by-value struct: the round loop reads them
+// through a pointer laundered per lap, so no argument is held in registers
+// across the loop (each lap reloads what it uses, as one pass would).
+struct LapKArgs {
+  const uint8_t *seqs;
+  const int64_t *offs;
+  int32_t G, GZ, NC, CH, YR, ZR;
+  uint8_t *yf_base, *zf_base;
+  LapRounds rd;
+  int32_t *prog;
+  uint32_t *err;
+  int32_t *scores, *mon;
+  PencilArgs pa;
+  uint32_t epoch, spin_limit;
+  int32_t L0, L1;
+  uint8_t *yf_out;
+  int32_t *prog_in;
+  unsigned long long *trace;
+  LitArgs lit;
+};
+// A kernarg-segment struct, word by word (scalar loads into registers)
+template <class T>
+__device__ __forceinline__ T kload(const __attribute__((address_space(4))) T &src) {
+  static_assert(sizeof(T) % 4 == 0, "word-sized");
+  T r;
+  uint32_t *d = (uint32_t *)&r;
+  const __attribute__((address_space(4))) uint32_t *w = (const __attribute__((address_space(4))) uint32_t *)&src;
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) d[i] = w[i];
+  return r;
+}
 template <int M, int NW, bool F16, bool SOP, bool CHK, bool SYS = false, bool LIT = false>
-__global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_kernel(
-    const uint8_t *__restrict__ seqs, const int64_t *__restrict__ offs, int32_t G, int32_t GZ,
-    int32_t NC, int32_t CH, int32_t YR, int32_t ZR, uint8_t *__restrict__ yf_base,
-    uint8_t *__restrict__ zf_base, LapRounds rd, int32_t *__restrict__ prog, uint32_t *__restrict__ err,
-    int32_t *__restrict__ scores, int32_t *__restrict__ mon, PencilArgs pa, uint32_t epoch,
-    uint32_t spin_limit, int32_t L0, int32_t L1, uint8_t *__restrict__ yf_out,
-    int32_t *__restrict__ prog_in,
-    unsigned long long *__restrict__ trace, LitArgs lit) {
+__global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_kernel(const LapKArgs ka) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   static_assert(!(CHK && F16), "the checked kernel runs the int16 form");
   static_assert(!(CHK && SYS), "a split cube runs the unchecked forms");
@@ -470,7 +495,40 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
   // block -> (lap, column): column c = tri*GZ + q (one z-tile of one triple), block
   // b = 8 * (L*CH + c/8) + c%8 -- a column's laps share b % 8 (one XCD), and
   // every producer ((L-1, c), (L, c-1)) has a lower block index than its consumer
-  const int32_t b = blockIdx.x, slot = b >> 3;
+  // Dispatch rounds are a loop, not a hope: the grid holds one round (every
+  // workgroup resident), and physical block p runs the logical blocks of
+  // slots p/8, p/8 + SX, p/8 + 2 SX, ... of its XCD one after another -- lap
+  // order per physical workgroup whatever the dispatcher does, and a slot's
+  // next lap starts the moment its previous one ends. One round: one pass.
+  typedef const __attribute__((address_space(4))) LapKArgs KargPtr;  // the kernarg segment (scalar loads)
+  auto lap_body = [&](const int32_t slot) {
+  // ka sits at offset 0 of the kernarg segment (its only explicit argument);
+  // taking &ka would copy it to private memory and make every field divergent
+  KargPtr *kap = (KargPtr *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(kap));
+  KargPtr &A = *kap;
+  const uint8_t *__restrict__ seqs = A.seqs;
+  const int64_t *__restrict__ offs = A.offs;
+  const int32_t G = A.G, GZ = A.GZ, NC = A.NC, CH = A.CH, YR = A.YR, ZR = A.ZR;
+  uint8_t *__restrict__ yf_base = A.yf_base, *__restrict__ zf_base = A.zf_base;
+  const LapRounds rd = kload(A.rd);
+  int32_t *__restrict__ prog = A.prog;
+  uint32_t *__restrict__ err = A.err;
+  int32_t *__restrict__ scores = A.scores, *__restrict__ mon = A.mon;
+  const PencilArgs pa = kload(A.pa);
+  const uint32_t epoch = A.epoch, spin_limit = A.spin_limit;
+  const int32_t L0 = A.L0, L1 = A.L1;
+  uint8_t *__restrict__ yf_out = A.yf_out;
+  int32_t *__restrict__ prog_in = A.prog_in;
+  unsigned long long *__restrict__ trace = A.trace;
+  const LitArgs lit = kload(A.lit);
+  const int32_t b = 8 * slot + (int32_t)(blockIdx.x & 7);  // logical block
+  // the lane / thread index laundered per lap: otherwise the compiler hoists
+  // every per-lane address out of the round loop and keeps it live across
+  // the whole body (+20 VGPRs, measured), where one pass rematerialises them
+  int32_t tid = (int32_t)threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63;
   const int32_t L = L0 + slot / CH, col = (slot % CH) * 8 + (b & 7);
   if (col >= NC || L >= L1) return;  // padding block
   const int32_t tri = col / GZ, q = col % GZ;
@@ -480,7 +538,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
   const int32_t nlap = (lb + RW - 1) / RW, ntile = (lc + ZT - 1) / ZT;
   if (L >= nlap || q >= ntile) return;  // beyond this triple's own laps / tiles
   auto stamp = [&](int s, unsigned long long v) {
-    if (trace != nullptr && threadIdx.x == 0) trace[(int64_t)b * LAP_TRACE_SLOTS + s] = v;
+    if (trace != nullptr && tid == 0) trace[(int64_t)b * LAP_TRACE_SLOTS + s] = v;
   };
   auto now = [&]() {
     unsigned long long v;
@@ -566,26 +624,26 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
 
   // ---- A code pairs, zeroed words
   const int32_t na = lap_na(la, M, NW, LIT);
-  for (int j = threadIdx.x; j < na; j += 64 * (NW + 1)) {
+  for (int j = tid; j < na; j += 64 * (NW + 1)) {
     const int x0 = j - OFF, x1 = j - OFF - 1;
     const uint32_t c0 = (x0 >= 0 && x0 < la) ? SYM0 << tsa_sym(seqs, o0 + x0, pa.packed) : 0u;
     const uint32_t c1 = (x1 >= 0 && x1 < la) ? SYM0 << tsa_sym(seqs, o0 + x1, pa.packed) : 0u;
     sA2[j] = c0 | (c1 << 16);
   }
-  if (threadIdx.x < 16) wd[threadIdx.x] = 0;
+  if (tid < 16) wd[tid] = 0;
   // face records, so a lap-0 wave 0 / tile-0 wave reads its y / z inputs the
   // same way as any other (no branch in the step): y {Iy, Ixy | Iyz, best} low
   // halves (wave 0's perm format), z {Iz, -, Ixz, - | Iyz, -, M, -}
-  for (int j = threadIdx.x; j < M * 64; j += 64 * (NW + 1))
+  for (int j = tid; j < M * 64; j += 64 * (NW + 1))
     ((uint4 *)yface)[j] = make_uint4((pa.f_single & 0xFFFFu) | (pa.f_pair & 0xFFFF0000u), 0u,
                                      pa.f_pair & 0xFFFFu, 0u);
-  if (threadIdx.x < 2 * NW)
-    ((uint4 *)zface)[threadIdx.x] = (threadIdx.x & 1) ? make_uint4(pa.f_pair, 0u, 0u, 0u)
+  if (tid < 2 * NW)
+    ((uint4 *)zface)[tid] = (tid & 1) ? make_uint4(pa.f_pair, 0u, 0u, 0u)
                                                       : make_uint4(pa.f_single, 0u, pa.f_pair, 0u);
-  pw[threadIdx.x] = 0;  // blockDim = 64 (NW + 1): one word per thread
+  pw[tid] = 0;  // blockDim = 64 (NW + 1): one word per thread
   // the wave-to-wave rings: step 0 reads slot K-1 before any write (its cells
   // are not real, but the checked kernel's monitor must not see stale LDS)
-  for (int j = threadIdx.x; j < (NW - 1) * K * SLOT / 16; j += 64 * (NW + 1))
+  for (int j = tid; j < (NW - 1) * K * SLOT / 16; j += 64 * (NW + 1))
     ((uint4 *)xr)[j] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
 
@@ -1166,7 +1224,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
     if (trace != nullptr) {
       const unsigned long long clk1 = __builtin_amdgcn_s_memtime();
       stamp(2, now());
-      if (threadIdx.x == 0) {
+      if (tid == 0) {
         trace[(int64_t)b * LAP_TRACE_SLOTS + 5] = n_wait;
         trace[(int64_t)b * LAP_TRACE_SLOTS + 6] = clk1 - clk0;
       }
@@ -1203,19 +1261,19 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // the final cell and the loader's counters are in LDS
-  if (trace != nullptr && threadIdx.x == 0) {
+  if (trace != nullptr && tid == 0) {
     trace[(int64_t)b * LAP_TRACE_SLOTS + 4] = (unsigned long long)w_stall[0];
     trace[(int64_t)b * LAP_TRACE_SLOTS + 7] = (unsigned long long)w_bp[0];
   }
   if constexpr (LIT) {
     if (final_wg) {  // block-uniform: the final cell's 7-tuple, unshifted, and its MAX7
       const int32_t kf = k_f, hf = r_f & 1;
-      if (threadIdx.x < 7) {
-        const uint32_t v = fin[(threadIdx.x * M + kf % M) * 64 + kf / M];
-        fin[7 * M * 64 + threadIdx.x] = (uint32_t)((int32_t)(int16_t)(uint16_t)(hf ? (v >> 16) : (v & 0xFFFF)) >> lit.sh);
+      if (tid < 7) {
+        const uint32_t v = fin[(tid * M + kf % M) * 64 + kf / M];
+        fin[7 * M * 64 + tid] = (uint32_t)((int32_t)(int16_t)(uint16_t)(hf ? (v >> 16) : (v & 0xFFFF)) >> lit.sh);
       }
       __syncthreads();
-      if (threadIdx.x == 0) {
+      if (tid == 0) {
         const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, SCOPE) == epoch;
         int32_t best = (int32_t)fin[7 * M * 64];
         for (int k = 1; k < 7; ++k) best = max(best, (int32_t)fin[7 * M * 64 + k]);
@@ -1224,7 +1282,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
           for (int k = 0; k < 7; ++k) mon[7 * (int64_t)tri + k] = (int32_t)fin[7 * M * 64 + k];
       }
     }
-  } else if (final_wg && threadIdx.x == 0) {
+  } else if (final_wg && tid == 0) {
     const int32_t kf = k_f, hf = r_f & 1;
     const uint32_t v = fin[(kf % M) * 64 + kf / M];
     const uint16_t hb = (uint16_t)(hf ? (v >> 16) : (v & 0xFFFF));
@@ -1233,6 +1291,13 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
     const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, SCOPE) == epoch;
     scores[tri] = bad ? TSA_SCORE_INVALID
                       : F16 ? (int32_t)(float)__builtin_bit_cast(_Float16, hb) : (int32_t)(int16_t)hb;
+  }
+  };
+  KargPtr *kout = (KargPtr *)__builtin_amdgcn_kernarg_segment_ptr();
+  const int32_t slots = (kout->L1 - kout->L0) * kout->CH, sx = kout->rd.SX;  // logical slots per XCD
+  for (int32_t slot = (int32_t)(blockIdx.x >> 3); slot < slots; slot += sx) {
+    lap_body(slot);
+    __syncthreads();  // the next lap re-initialises this workgroup's LDS
   }
 }
 
@@ -1278,6 +1343,11 @@ static DevInfo dev_info() {
 // checked (CHK) and split (SYS) ones too, whose register counts can differ
 // from the plain kernel's -- so the grid plan holds whichever of them runs.
 int lap_simd_blocks_per_cu(int M, int NW, bool f16, bool sop, bool lit) {
+  // memo (value + 1; 0 = not yet computed): the table scans run per plan
+  static std::atomic<int> memo[4][2][2][2][2];
+  const int mi = M == 1 ? 0 : M == 2 ? 1 : M == 4 ? 2 : 3;
+  std::atomic<int> &slot = memo[mi][NW == 8][f16][sop][lit];
+  if (const int v = slot.load(std::memory_order_relaxed)) return v - 1;
   int sgpr = -1, vgpr = -1;
   for (int chk = 0; chk < 2; ++chk)
     for (int sys = 0; sys < 2; ++sys) {
@@ -1288,20 +1358,41 @@ int lap_simd_blocks_per_cu(int M, int NW, bool f16, bool sop, bool lit) {
       vgpr = std::max(vgpr, kernel_vgpr_max(prefix));
     }
   const int waves = std::min(sgpr_waves_per_simd(sgpr < 0 ? 112 : sgpr), vgpr_waves_per_simd(vgpr < 0 ? 256 : vgpr));
-  return waves / ((NW + 1 + 3) / 4);
+  const int r = waves / ((NW + 1 + 3) / 4);
+  slot.store(r + 1, std::memory_order_relaxed);
+  return r;
 }
 // Workgroups of one instantiation a CU holds, from the HIP occupancy API on the
 // real kernel (VGPRs, LDS) capped by the SGPR bound (the API reads one block
 // high at 81-112 SGPRs); without a device, the LDS / wave-slot model.
+// Memoized per (device, LDS bytes): a single-cube call plans a dozen
+// geometries, and each occupancy query is host latency on that call.
 template <int M, int NW, bool F16, bool SOP, bool LIT = false>
 static int lap_blocks_per_cu_t(size_t lds) {
+  struct Entry {
+    int dev;
+    size_t lds;
+    int nb;
+  };
+  static std::mutex mu;
+  static std::vector<Entry> memo;
   int nb = 0;
   int dev = -1;
   const int sg = lap_simd_blocks_per_cu(M, NW, F16, SOP, LIT);
-  if (hipGetDevice(&dev) == hipSuccess &&
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lap_kernel<M, NW, F16, SOP, false, false, LIT>,
-                                                   64 * (NW + 1), lds) == hipSuccess)
-    return std::min(nb, sg);
+  if (hipGetDevice(&dev) == hipSuccess) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      for (const Entry &e : memo)
+        if (e.dev == dev && e.lds == lds) return e.nb;
+    }
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lap_kernel<M, NW, F16, SOP, false, false, LIT>,
+                                                     64 * (NW + 1), lds) == hipSuccess) {
+      nb = std::min(nb, sg);
+      std::lock_guard<std::mutex> g(mu);
+      if (memo.size() < 4096) memo.push_back(Entry{dev, lds, nb});
+      return nb;
+    }
+  }
   return (int)std::min<size_t>(std::min<size_t>(LDS_MAX / std::max<size_t>(lds, 1), 32 / (NW + 1)), sg);
 }
 template <int M, int NW, bool SOP>
@@ -1391,6 +1482,7 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   // dispatch rounds: boundary rings for producers whose consumer is in a later
   // round (kernel: y_bidx / z_bidx); one round, or full rings: none
   g.SX = (full_rings || g.waves <= 1 || per_cu <= 0) ? (1 << 30) : (int32_t)slots_xcd;
+  g.grid = g.SX < (1 << 30) ? 8 * (int64_t)g.SX : g.blocks;  // one resident round, looped
   g.KBY = g.KBZ = 0;
   if (g.SX < (1 << 30)) {
     if (g.CH >= g.SX) {
@@ -1418,10 +1510,19 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   const int64_t wg_cu = std::max<int64_t>(1, std::min<int64_t>(per_cu, (wg_per_xcd + xcd_cus - 1) / xcd_cus));
   const double steps = (double)(g.G - 1) * (YOFF + LPD + 3) + (double)(g.GZ - 1) * (ZT + LPD + 2) +
                        (double)(max_la + YOFF + ZT);
-  const double chain = steps * lap_step_us(M, NW, wg_cu, lit);
-  // a later round starts as the earlier one's workgroups finish: 1024^3 (M = 2,
-  // two rounds of one workgroup per CU) runs 3.04 ms against a 2.25 ms chain
-  g.est_us = chain * (1.0 + 0.35 * (double)(std::max<int64_t>(g.waves, 1) - 1));
+  const double step = lap_step_us(M, NW, wg_cu, lit);
+  const double chain = steps * step;
+  // a slot's lap of round r + 1 starts when its lap of round r ends: one lap's
+  // steps after its start, against (laps per round - 1) hand-offs of the chain
+  // -- a round boundary delays the chain by the difference (round 2 of 1024^3,
+  // M = 2, one workgroup per CU: 3.04 ms measured against a 2.25 ms chain)
+  double delay = 0.0;
+  if (g.waves > 1) {
+    const double lpr = std::max(1.0, (double)g.SX / (double)g.CH);  // laps of a column per round
+    const double lap_steps = (double)(max_la + YOFF + ZT) + (double)(g.GZ - 1) * (ZT + LPD + 2) / lpr;
+    delay = std::max(0.0, lap_steps - (lpr - 1.0) * (YOFF + LPD + 3)) * step * 1.5;
+  }
+  g.est_us = chain + (double)(std::max<int64_t>(g.waves, 1) - 1) * delay;
   return g;
 }
 
@@ -1436,9 +1537,9 @@ LapGeom lap_geom_chunked(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_
   for (int32_t k = n;; k = (k + 1) / 2) {
     const int32_t kk = forced > 0 ? std::min(forced, n) : k;
     LapGeom g = lap_geom(kk, max_la, max_lb, max_lc, M, NW, false, f16, sop, lit);
-    // rounds with two workgroups per CU: a later round's workgroups start out
-    // of chain order as slots free (lap_choice)
-    if (g.ok && g.waves <= LAP_MAX_WAVES && !(g.waves > 1 && g.per_cu > 1)) {
+    // rounds run as each workgroup's loop over its slots (lap_kernel), in lap
+    // order whatever the workgroups per CU
+    if (g.ok && g.waves <= LAP_MAX_WAVES) {
       const int64_t launches = (n + kk - 1) / kk;
       g.chunk = kk < n ? kk : 0;
       g.est_us = g.est_us * (double)launches + 5.0 * (double)(launches - 1);
@@ -1491,8 +1592,7 @@ static int launch_lap_fn(LapKernelFn kfn, int NW, const uint8_t *d_seqs, const i
   if (g.prog_bytes > ga.prog_bytes || g.yf_bytes > ga.yf_bytes || g.zf_bytes > ga.zf_bytes ||
       g.yb_bytes > ga.yb_bytes || g.zb_bytes > ga.zb_bytes)
     return TSA_EINTERNAL;  // a chunk's regions must fit the batch's
-  if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)g.lds) != hipSuccess)
+  if (set_dynamic_lds((const void *)kfn, g.lds) != hipSuccess)
     return TSA_EDEVICE;
   int32_t *prog = (int32_t *)d_ws;
   uint32_t *err = lap_err_word(ga, n, d_ws);
@@ -1511,10 +1611,9 @@ static int launch_lap_fn(LapKernelFn kfn, int NW, const uint8_t *d_seqs, const i
   if (trace && hipMemsetAsync(trace, 0, tbytes, stream) != hipSuccess)
     return TSA_EDEVICE;
   const uint32_t epoch = lap_next_epoch();
-  hipLaunchKernelGGL(kfn, dim3((uint32_t)g.blocks), dim3(64 * (NW + 1)), g.lds, stream, d_seqs,
-                     d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, rd, prog, err,
-                     d_scores, mon, pa,
-                     epoch, lap_spin_limit(), 0, g.G, yf, prog, trace, lit);
+  const LapKArgs ka{d_seqs, d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, rd, prog, err,
+                    d_scores, mon, pa, epoch, lap_spin_limit(), 0, g.G, yf, prog, trace, lit};
+  hipLaunchKernelGGL(kfn, dim3((uint32_t)g.grid), dim3(64 * (NW + 1)), g.lds, stream, ka);
   if (chk) {
     if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
     hipLaunchKernelGGL(lap_certify, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, mon, n,
@@ -1625,8 +1724,7 @@ static int launch_split_fn(LapKernelFn kfn, int NW, const LapGeom &g, const Penc
   for (int p = 0; p < np; ++p) {
     const LapPart &q = parts[p];
     if (hipSetDevice(q.device) != hipSuccess) return TSA_EDEVICE;
-    if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)g.lds) != hipSuccess)
+    if (set_dynamic_lds((const void *)kfn, g.lds) != hipSuccess)
       return TSA_EDEVICE;
     int32_t *prog = (int32_t *)q.d_ws;
     uint8_t *yf = (uint8_t *)q.d_ws + g.prog_bytes;
@@ -1634,11 +1732,10 @@ static int launch_split_fn(LapKernelFn kfn, int NW, const LapGeom &g, const Penc
     uint8_t *yf_out = p + 1 < np ? (uint8_t *)parts[p + 1].d_ws + g.prog_bytes : yf;
     int32_t *prog_in = p > 0 ? (int32_t *)parts[p - 1].d_ws : prog;
     const int64_t blocks = (int64_t)(q.L1 - q.L0) * g.CH * 8;
-    hipLaunchKernelGGL(kfn, dim3((uint32_t)blocks), dim3(64 * (NW + 1)), g.lds, q.stream, q.d_seqs,
-                       q.d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, lap_rounds(g, q.d_ws), prog,
-                       d_err, d_score,
-                       (int32_t *)nullptr, pa, epoch, spin, q.L0, q.L1, yf_out, prog_in,
-                       (unsigned long long *)nullptr, lit);
+    const LapKArgs ka{q.d_seqs, q.d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, lap_rounds(g, q.d_ws),
+                      prog, d_err, d_score, (int32_t *)nullptr, pa, epoch, spin, q.L0, q.L1, yf_out, prog_in,
+                      (unsigned long long *)nullptr, lit};
+    hipLaunchKernelGGL(kfn, dim3((uint32_t)blocks), dim3(64 * (NW + 1)), g.lds, q.stream, ka);
     if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
   }
   return TSA_OK;

@@ -536,7 +536,7 @@ static int launch_lit(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
                       hipStream_t stream) {
   const int32_t lds_a = 4 * (g.P + 128 * M), lds_b = 4 * ((max_lb + 4) & ~3);
   auto kfn = literal_kernel<M, SOP>;
-  if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)g.lds) != hipSuccess)
+  if (set_dynamic_lds((const void *)kfn, g.lds) != hipSuccess)
     return TSA_EDEVICE;
   const int grid = n < 65535 ? n : 65535;
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * LIT_NW), g.lds, stream, d_seqs, d_offsets, n, g.P, g.R, lds_a,

@@ -133,13 +133,12 @@ static double helix_est(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_l
 
 // The lap kernel's geometry if it should run, else .ok = false (helix).
 // Resident grids (waves == 1) are safe: every workgroup runs at once, so a
-// consumer waiting for a record never holds a slot its producer needs. A grid
-// beyond the resident slots runs in dispatch rounds: producers always have
-// lower block indices than their consumers, so with blocks dispatched in order
-// per XCD (observed at 768^3 / 1024^3, where the M = 2 grid has always run
-// two rounds of one workgroup per CU; not promised by HIP) a consumer's
-// producer is running or done, and a producer never waits for a consumer of
-// a later round (boundary rings, lap_geom); every wait is bounded.
+// consumer waiting for a record never holds a slot its producer needs. A cube
+// beyond the resident slots runs in rounds inside one resident grid: each
+// workgroup loops over its slot's laps in lap order (lap_kernel), so a
+// consumer's producer is always running or done, and a producer never waits
+// for a consumer of a later round (boundary rings, lap_geom); every wait is
+// bounded.
 static LapGeom lap_choice(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc,
                           LapPolicy lap, bool f16, bool sop, bool need = false) {
   LapGeom none{};
@@ -154,15 +153,11 @@ static LapGeom lap_choice(int32_t n, int32_t max_la, int32_t max_lb, int32_t max
   LapGeom best = none;
   for (int M = m_lo; M <= m_hi; M *= 2) {
     for (int NW = nw_lo; NW <= nw_hi; NW *= 2) {
-      // a grid of several dispatch rounds runs with boundary rings (lap_geom)
-      // on both paths: it relies on per-XCD in-order dispatch, measured
-      // (DESIGN.md 4.4); a hand-off that times out still reports, never hangs.
-      // Rounds with two workgroups per CU are refused (a later round's
-      // workgroups start out of chain order as slots free, lags reach ~1100
-      // steps and the slim rings stall: 1024^3 M = 1 NW = 8, 37206
-      // back-pressure waits, timed out; with one per CU they start in chain
-      // order, M = 2: none, 3.00 ms); a larger batch runs as chunks of
-      // triples, one launch each (lap_geom_chunked)
+      // several rounds run as the resident workgroups' loops with boundary
+      // rings (lap_geom), at any workgroups per CU (when the hardware
+      // dispatcher ran round 2, two per CU started out of chain order and
+      // timed out); a larger batch runs as chunks of triples, one launch
+      // each (lap_geom_chunked)
       const LapGeom g = lap_geom_chunked(n, max_la, max_lb, max_lc, M, NW, f16, sop);
       if (!g.ok) continue;
       if (!best.ok || g.est_us < best.est_us) best = g;
@@ -845,8 +840,7 @@ static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
   auto kfn = vs ? (two ? pencil_kernel<M, NW, F16, SOP, M == 1, VSOK> : pencil_kernel<M, NW, F16, SOP, false, VSOK>)
                 : (two ? pencil_kernel<M, NW, F16, SOP, M == 1, false> : pencil_kernel<M, NW, F16, SOP, false, false>);
   if (lds > LDS_MAX) return TSA_EINVAL;
-  if (hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)lds) != hipSuccess)
+  if (set_dynamic_lds((const void *)kfn, lds) != hipSuccess)
     return TSA_EDEVICE;
   const int32_t units = two ? (n + 1) / 2 : n;
   const int grid = units < 65535 ? units : 65535;

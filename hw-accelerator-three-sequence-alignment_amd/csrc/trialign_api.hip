@@ -187,6 +187,34 @@ int tsa_validate(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb, con
 
 namespace tsa {
 
+hipError_t set_dynamic_lds(const void *fn, size_t lds) {
+  struct Entry {
+    const void *fn;
+    int dev;
+    size_t lds;
+  };
+  static std::mutex mu;
+  static std::vector<Entry> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    for (const Entry &e : done)
+      if (e.fn == fn && e.dev == dev && e.lds >= lds) return hipSuccess;
+  }
+  const hipError_t rc = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (rc == hipSuccess) {
+    std::lock_guard<std::mutex> g(mu);
+    for (Entry &e : done)
+      if (e.fn == fn && e.dev == dev) {
+        e.lds = std::max(e.lds, lds);
+        return rc;
+      }
+    done.push_back(Entry{fn, dev, lds});
+  }
+  return rc;
+}
+
 // Is the factored (pencil) arithmetic bit-identical to the literal RTL form
 // for every triple of these lengths? Two separate conditions:
 //  (1) no candidate can wrap at score_bits -- the bare bound, which already

@@ -48,6 +48,12 @@ Range value_bound(const tsa_params *p, int64_t la, int64_t lb, int64_t lc);
 // below a state (cdrop), for value_bound and the checked kernel.
 void bound_drops(const tsa_params *p, int64_t *drop, int64_t *cdrop);
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) for `fn` on the current
+// device, skipped when an earlier call on that device already allowed at
+// least `lds` bytes (a per-launch attribute call is host latency on every
+// single-cube call). hipSuccess or the HIP error.
+hipError_t set_dynamic_lds(const void *fn, size_t lds);
+
 // Row stride (cells) of a (y,z) plane with lc+1 columns.
 inline int64_t plane_ldz(int64_t lc) { return lc + 1; }
 

@@ -84,6 +84,9 @@ def main():
                "gcups": round(n * L ** 3 / (med * 1e-3) / 1e9, 2)}
         if ref is not None:
             rec["parity_ok"] = bool((scores[v][idx] == ref).all())
+        # every variant must score the batch identically (and never the
+        # TSA_SCORE_INVALID of a timed-out hand-off)
+        rec["agree"] = bool((scores[v] == scores[args.variants[0]]).all()) and int(scores[v].min()) > -(1 << 30)
         print(json.dumps(rec), flush=True)
 
 
