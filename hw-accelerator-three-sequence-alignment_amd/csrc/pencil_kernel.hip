@@ -415,6 +415,11 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     int32_t st_row = 0;                          // ring row written at step t (last wave)
     uint32_t abase = a_lane;                     // VS: A address of the group's first step
 
+    // VS: the step whose cell is the final one, in this wave (-1: none)
+    const int32_t t_fin = w == w_f ? T - 1 : -1;
+    // the x = 1 mask kept from the even step of a pair (step, MASK_PAIRS)
+    constexpr bool MASK_PAIRS = VS && M == 2 && HSK == 2 && TSA_HM_TRACK;
+    uint32_t m1_pair = 0u;
     // One step; PH = t & 1 picks the register roles and the LDS record slots,
     // ROLE the wave's place in the lap (0: wave 0, reads the ring; 2: the last
     // wave, writes it; 1: the others), so the loop body has no role branches.
@@ -468,7 +473,16 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         pos_split<M>(xpos0, ls, is, hs);
 #if TSA_HM_TRACK
         uint32_t m1;
-        asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(m1) : "v"(hmCur), "s"(1ull << ls));
+        // M = 2, skew 2: xpos0 has t's parity, so the odd step of a pair
+        // injects the same lane and half as the even one (register 1 after
+        // register 0; the half-mask events and the lap wrap fall on even
+        // xpos0, between pairs): its mask is the even step's
+        if constexpr (MASK_PAIRS && (PQ & 1)) {
+          m1 = m1_pair;
+        } else {
+          asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(m1) : "v"(hmCur), "s"(1ull << ls));
+          if constexpr (MASK_PAIRS) m1_pair = m1;
+        }
 #elif TSA_LANE_MASK
         const uint32_t m1 = lane_half_mask(ls, hs, hmLo, hmHi);
 #else
@@ -533,7 +547,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         if (t == t_f && w == w_f) fin[lane] = oBest[0];
         if (t == t_f1 && w == w_f1) fin[64 + lane] = oBest[0];
       } else if constexpr (VS) {  // the four-step loop runs past T: the final step is tested
-        if (t == T - 1 && w == w_f) {
+        if (t == t_fin) {  // (peeling the last group instead trips a gfx950 backend bug)
 #pragma unroll
           for (int i = 0; i < M; ++i) fin[i * 64 + lane] = oBest[i];
         }
