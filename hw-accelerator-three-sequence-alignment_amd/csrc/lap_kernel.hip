@@ -139,6 +139,12 @@ __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel)
 __device__ __forceinline__ uint32_t rows2(uint32_t own, uint32_t above) {
   return __builtin_amdgcn_alignbit(own, above, 16);
 }
+// f16 bits of the integer lam * v in both halves (V-space face values; exact
+// below 2048 in magnitude, which the host's range check guarantees)
+__device__ __forceinline__ uint32_t lam_bits(int32_t lam, int32_t v) {
+  const _Float16 h = (_Float16)(float)(lam * v);
+  return (uint32_t)__builtin_bit_cast(uint16_t, h) * 0x00010001u;
+}
 // A wave-uniform 64-bit lane mask, forced into an SGPR pair (the compiler may
 // compute a uniform shift in VALU and hand the VGPR pair to an "s" operand)
 __device__ __forceinline__ uint64_t sgpr64(uint64_t v) {
@@ -240,6 +246,72 @@ __device__ __forceinline__ void lap_post_f16(const PencilArgs &pa, const uint32_
     oIxy[i] = U(hmax(yE, H(p.N4[i])));
     oIyz[i] = U(hmax(yE, H(p.N5[i])));
     oIxz[i] = U(hmax(y - O, H(p.N6[i])));
+  }
+}
+// The V-space cell (cell_messages_vs: every value of cell (x,y,z) shifted by
+// lam (x+y+z), lam = GE = -MISMATCH) split at the row above the same way.
+// With Gx = max(Y, gx), Gz = max(Y, gz), best = max(Y, W) and DO = GO - GE
+// >= 0, CP = GO + MISMATCH + lam >= lam (tests/test_cell_algebra.py):
+//   W  = max(gx, Gy, XY', M'),  gx = max(Z, YZ'), gz = max(X, XY'), Gy = max(X, Z, XZ')
+//   Ixy' = max(Y, NXY),      NXY = max(gz, W - DO)
+//   Iyz' = max(Y, NYZ),      NYZ = max(gx, W - DO)
+//   Ixz' = max(Y - DO, NXZ), NXZ = max(Gy, W - DO)
+//   Ix'  = max(Y - CP, N1),  N1 = max(X - lam, NXY - CP, NXZ - CP)
+//   Iy'  = max(Y - lam, N2), N2 = max(NXY - CP, NYZ - CP)
+//   Iz'  = max(Y - CP, N3),  N3 = max(Z - lam, NYZ - CP, NXZ - CP)
+// 23 instructions per pair before the record lands, 10 after (the message
+// form: 32 + 11). LapPre slots: N4 = NXY, N5 = NYZ, N6 = NXZ.
+template <int M, bool SOP>
+__device__ __forceinline__ void lap_pre_vs(const uint32_t (&a)[M], const uint32_t (&b)[M],
+                                           const uint32_t (&c)[M], const uint32_t (&SBC)[M],
+                                           const uint32_t (&K)[M], const uint32_t (&DMC)[M],
+                                           const uint32_t (&DMB)[M], const PencilArgs &pa,
+                                           const uint32_t (&inIx)[M], const uint32_t (&inIz)[M],
+                                           const uint32_t (&inIxy)[M], const uint32_t (&inIyz)[M],
+                                           const uint32_t (&inIxz)[M], const uint32_t (&inM)[M],
+                                           LapPre<M> &p) {
+  const h2 LAM = H(pa.v_lam), CP = H(pa.v_cP), DO = H(pa.v_dO);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const h2 eab = H(a[i] & b[i]), eac = H(a[i] & c[i]), DMCi = H(DMC[i]), DMBi = H(DMB[i]);
+    const h2 sXY = hfma(eab, DMBi, H(inIxy[i]));  // src/PE_1cyc.v:159-161 (+mismatch folded)
+    const h2 sXZ = hfma(eac, DMCi, H(inIxz[i]));
+    const h2 sYZ = H(inIyz[i]) + H(SBC[i]);
+    h2 sM;                                        // src/PE_1cyc.v:162
+    if constexpr (SOP) sM = hfma(eab, DMBi, hfma(eac, DMCi, H(inM[i]))) + H(K[i]);
+    else sM = hfma(eab, H(K[i]), H(inM[i]));      // ne + 3 lam = 0
+    const h2 X = H(inIx[i]), Z = H(inIz[i]);
+    const h2 gx = hmax(Z, sYZ), gz = hmax(X, sXY), Gy = vmax3(X, Z, sXZ);
+    const h2 W = vmax3(gx, Gy, hmax(sXY, sM));
+    const h2 WD = W - DO;
+    const h2 NXY = hmax(gz, WD), NYZ = hmax(gx, WD), NXZ = hmax(Gy, WD);
+    const h2 qXY = NXY - CP, qYZ = NYZ - CP, qXZ = NXZ - CP;
+    p.W[i] = U(W);
+    p.N4[i] = U(NXY);
+    p.N5[i] = U(NYZ);
+    p.N6[i] = U(NXZ);
+    p.N1[i] = U(vmax3(X - LAM, qXY, qXZ));
+    p.N2[i] = U(hmax(qXY, qYZ));
+    p.N3[i] = U(vmax3(Z - LAM, qYZ, qXZ));
+  }
+}
+template <int M>
+__device__ __forceinline__ void lap_post_vs(const PencilArgs &pa, const uint32_t (&Y)[M],
+                                            const LapPre<M> &p, uint32_t (&nIx)[M],
+                                            uint32_t (&oIy)[M], uint32_t (&oIz)[M],
+                                            uint32_t (&oIxy)[M], uint32_t (&oIyz)[M],
+                                            uint32_t (&oIxz)[M], uint32_t (&oBest)[M]) {
+  const h2 LAM = H(pa.v_lam), CP = H(pa.v_cP), DO = H(pa.v_dO);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    const h2 y = H(Y[i]), yCP = y - CP;
+    oBest[i] = U(hmax(y, H(p.W[i])));
+    oIxy[i] = U(hmax(y, H(p.N4[i])));
+    oIyz[i] = U(hmax(y, H(p.N5[i])));
+    oIxz[i] = U(hmax(y - DO, H(p.N6[i])));
+    nIx[i] = U(hmax(yCP, H(p.N1[i])));
+    oIy[i] = U(hmax(y - LAM, H(p.N2[i])));
+    oIz[i] = U(hmax(yCP, H(p.N3[i])));
   }
 }
 // int16 form (two's complement halves): the same split of cell_messages
@@ -465,12 +537,19 @@ __device__ __forceinline__ T kload(const __attribute__((address_space(4))) T &sr
   for (int i = 0; i < (int)(sizeof(T) / 4); ++i) d[i] = w[i];
   return r;
 }
-template <int M, int NW, bool F16, bool SOP, bool CHK, bool SYS = false, bool LIT = false>
+// VS: the V-space f16 cell (lap_pre_vs), every value shifted by lam (x+y+z):
+// the faces become lam q (the x = 0 face injected at x = 1, the y = 0 / z = 0
+// faces written by the loader like the literal form's), the score shifted
+// back at the end.
+template <int M, int NW, bool F16, bool SOP, bool CHK, bool SYS = false, bool LIT = false, bool VS = false>
 __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_kernel(const LapKArgs ka) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   static_assert(!(CHK && F16), "the checked kernel runs the int16 form");
   static_assert(!(CHK && SYS), "a split cube runs the unchecked forms");
   static_assert(!(LIT && (F16 || CHK)), "the literal form: int16, unchecked");
+  static_assert(!VS || (F16 && !CHK && !LIT && !SYS), "V-space: the f16 single-device form");
+  // the loader writes the step-varying y = 0 / z = 0 faces (LIT, VS)
+  constexpr bool FACES = LIT || VS;
   constexpr int SCOPE = SYS ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
   constexpr int RW = 2 * NW, ZT = 64 * M, LPD = lap_pd(M), K = lap_k(M), K0 = lap_k0(M);
   constexpr int PAIR = 64 * REC_BYTES, SLOT = M * PAIR;
@@ -490,7 +569,6 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
   uint32_t *sA2 = fin + lap_fin_words(M, LIT);
   int32_t *const w_bp = wd + 9, *const w_abort = wd + 12, *const bpw = wd + 13, *const w_stall = wd + 15;
 
-  const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // w == NW: the loader
   // block -> (lap, column): column c = tri*GZ + q (one z-tile of one triple), block
   // b = 8 * (L*CH + c/8) + c%8 -- a column's laps share b % 8 (one XCD), and
@@ -720,6 +798,23 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
         return make_uint4(lit_face_pair(cv, lby2, lc1, lones), 0u, lit_face_m<SOP>(cv, a2, lby2, lc1, lones), 0u);
       return make_uint4(cv.fS[2], 0u, lit_face_pair(cv, a2, lc1, lones), 0u);
     };
+    // VS: the same faces as V-space values -- a face cell at coordinate sum
+    // q_f sends lam q_f to a pair target and to M, lam q_f - lam to a single
+    // target. Lap 0's record of step s (wave 0's low halves, rows 0 -> 1):
+    // Iy = lam (s + zoff + 1), Ixy = Iyz = best = lam (s + zoff + 2), the same
+    // on every lane (x + z is the step); tile 0's z record for step t = rz - ZT
+    // (position 0 of every wave): Iz = Iyz = M = lam (t + L RW + 2), Ixz one lam more
+    const int32_t zoff = q * ZT;
+    auto yface_vs = [&](int32_t s) -> uint4 {
+      const uint32_t f1 = lam_bits(pa.lam, s + zoff + 1) & 0xFFFFu, f2 = lam_bits(pa.lam, s + zoff + 2) & 0xFFFFu;
+      return make_uint4(f1 | (f2 << 16), 0u, f2 | (f2 << 16), 0u);
+    };
+    auto zface_vs = [&](int32_t rz) -> uint4 {
+      const int32_t t = rz - ZT;
+      const uint32_t g1 = lam_bits(pa.lam, t + L * RW + 2);
+      if (lane & 1) return make_uint4(g1, 0u, g1, 0u);                  // {Iyz, -, M, -}
+      return make_uint4(g1, 0u, lam_bits(pa.lam, t + L * RW + 3), 0u);  // {Iz, -, Ixz, -}
+    };
     auto tag_ok = [](u64 g, uint32_t tg) { return (uint32_t)(g >> 32) == tg; };
     auto y_ok = [&](int32_t s, const Fetch &f) {
       const uint32_t tg = lap_tag(epoch, s + YOFF);
@@ -769,13 +864,16 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
         if constexpr (LIT) {
           if (!zin) v = zface_lit(rz);
         }
+        if constexpr (VS) {
+          if (!zin) v = zface_vs(rz);
+        }
         lds_write16(zring + (rz & (LAP_ZL - 1)) * ZREC + lane * 16, v);
       }
     };
     int32_t seen_w0 = 0, seen_wl = 0;
     // prologue: z records ZT-2 .. ZT+ZA-1 (position 0's step-0 inputs and the
     // z reads of steps the loader's progress does not cover), checked now
-    if (zin || LIT) {  // (LIT tile 0: the z = 0 faces of those records)
+    if (zin || FACES) {  // (LIT / VS tile 0: the z = 0 faces of those records)
       for (int rz = ZT - 2; rz < ZT + ZA; ++rz) {
         Fetch f;
         f.z[0] = f.z[1] = 0;
@@ -814,6 +912,9 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
         if constexpr (LIT) {
           if (!yin) v = yface_lit(s, i);
         }
+        if constexpr (VS) {
+          if (!yin) v = yface_vs(s);
+        }
         lds_write16(dst + i * PAIR, v);
       }
       put_z(rz, f);
@@ -836,11 +937,23 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
     const int32_t y0 = L * RW + 2 * w;  // rows y0 (lo) and y0 + 1 (hi), 0-based
     const uint32_t bw = (y0 < lb ? SYM0 << tsa_sym(seqs, o1 + y0, pa.packed) : 0u) |
                         ((y0 + 1 < lb ? SYM0 << tsa_sym(seqs, o1 + y0 + 1, pa.packed) : 0u) << 16);
-    uint32_t bv[M], c[M], SBC[M], K_[M], DMC[M];
+    uint32_t bv[M], c[M], SBC[M], K_[M], DMC[M], DMB[M];
     uint32_t oIx[M], shIz[M], svIxy[M], svIyz[M], shIxz[2][M], svM[2][M];
     uint32_t pIy[M], pIxy[M], pIyz[M], pBest[M];  // this wave's record of the previous step
     {
       uint32_t one1 = 0x00010001u, sbcv = pa.h_sbc, kdv = pa.h_kd, k0v = pa.h_k0;
+      uint32_t dmb = 0u;
+      if constexpr (VS) {
+        // the [a=b] terms multiply b's one-hot code itself (a & b, no min):
+        // DMB = dm / code(b) and, RTL s3, K = (d0 + [b=c] d1) / code(b)
+        // (cell_messages_vs); both rows of the wave, one per half
+        dmb = dm_over_code(pa.dmf, bw);
+        if constexpr (!SOP) {
+          k0v = dm_over_code(pa.d0f, bw);
+          const uint32_t kb1 = dm_over_code(pa.d0f + pa.d1f, bw);
+          kdv = (((kb1 & 0xFFFFu) - (k0v & 0xFFFFu)) & 0xFFFFu) | ((((kb1 >> 16) - (k0v >> 16)) & 0xFFFFu) << 16);
+        }
+      }
       asm volatile("" : "+v"(one1), "+v"(sbcv), "+v"(kdv), "+v"(k0v));
       const int64_t oc = o2 + (int64_t)q * ZT;
 #pragma unroll
@@ -852,6 +965,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
         const uint32_t e01 = pk_eq1(bw, c[i], one1);
         SBC[i] = pk_mad(e01, sbcv, 0u);
         K_[i] = pk_mad(e01, kdv, k0v);
+        DMB[i] = dmb;
         oIx[i] = shIz[i] = pa.f_single;
         shIxz[0][i] = shIxz[1][i] = svIxy[i] = svIyz[i] = pa.f_pair;
         svM[0][i] = svM[1][i] = 0;
@@ -891,8 +1005,17 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
     asm volatile("" : "+v"(Q), "+v"(fsv), "+v"(fpv), "+v"(mlo), "+v"(mhi));
     const PencilArgs pv = F16 ? pa : pin_score_consts(pa);
     const uint32_t sel0 = lane == 0 ? 0x03020100u : 0x07060504u;  // lane 0: whole word from the face
+    // VS: the x = 0 face at the x = 1 cells of step t -- the low half's
+    // position t - 2w and the high half's one behind share x + y + z =
+    // t + L RW + zoff + 3, so one value for both: lam (t + L RW + zoff + 1)
+    // for Ix, Ixy, Ixz (one lam less for M: the previous step's)
+    uint32_t hx_cur = 0u, hx_prev = 0u;
+    if constexpr (VS) {
+      hx_cur = lam_bits(pa.lam, L * RW + q * ZT + 1);
+      hx_prev = lam_bits(pa.lam, L * RW + q * ZT);
+    }
     __syncthreads();  // the loader's prologue z records are in LDS
-    if (zin || LIT) {  // position 0 before step 0 (tools/lap_emu.py: the same initial shifts)
+    if (zin || FACES) {  // position 0 before step 0 (tools/lap_emu.py: the same initial shifts)
       const uint8_t *r1 = zring + ((ZT - 1) & (LAP_ZL - 1)) * ZREC + w * LAP_ZREC_WAVE;
       const uint8_t *r2 = zring + ((ZT - 2) & (LAP_ZL - 1)) * ZREC + w * LAP_ZREC_WAVE;
       const uint4 a0 = lds_read16(r1), a1 = lds_read16(r1 + 16);
@@ -912,12 +1035,12 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
       clk0 = __builtin_amdgcn_s_memtime();  // shader clock: the loop's cycles (slot 6)
     }
     // wave 0's y input: xr0 slot t % K0, or the face record (stride 0)
-    // (LIT: always the loader's, which writes the step-varying faces)
-    const uint8_t *const ysrc = ((yin || LIT) ? xr0 : yface) + lane * REC_BYTES;
-    const int32_t ystride = (yin || LIT) ? SLOT : 0;
+    // (LIT / VS: always the loader's, which writes the step-varying faces)
+    const uint8_t *const ysrc = ((yin || FACES) ? xr0 : yface) + lane * REC_BYTES;
+    const int32_t ystride = (yin || FACES) ? SLOT : 0;
     // position 0's z input: zring slot (t + ZT) % ZL, or the face record
-    const uint8_t *const zsrc = ((zin || LIT) ? zring : zface) + w * LAP_ZREC_WAVE;
-    const int32_t zstride = (zin || LIT) ? ZREC : 0;
+    const uint8_t *const zsrc = ((zin || FACES) ? zring : zface) + w * LAP_ZREC_WAVE;
+    const int32_t zstride = (zin || FACES) ? ZREC : 0;
     uint32_t a_nx[M];
     load_a<M>(a_lane, a_nx);
     // producer side: my consumers' progress (y: the lap below, via the last
@@ -972,7 +1095,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
 #endif
       const int32_t need = ROLE == 0 ? t + 1 : t;
       const int32_t *const pword = ROLE == 0 ? pw + 64 * NW : pw + 64 * (w - 1);
-      const bool waits = ROLE != 0 || yin || zin || LIT;
+      const bool waits = ROLE != 0 || yin || zin || FACES;
       const bool poll = waits && seen_in < need;
       int32_t fl_v = 0;
       if (poll)
@@ -1023,15 +1146,19 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
         uint32_t m0, m1;
         asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(m0) : "v"(mhi), "s"(mh));
         asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(m1) : "v"(m0), "v"(mlo), "s"(ml));
-        inIx[i] = vbfi(m1, fsv, inIx[i]);
-        inIxy[i] = vbfi(m1, fpv, inIxy[i]);
-        inIxz[i] = vbfi(m1, fpv, inIxz[i]);
-        inM[i] = vbfi(m1, 0u, inM[i]);
+        inIx[i] = vbfi(m1, VS ? hx_cur : fsv, inIx[i]);
+        inIxy[i] = vbfi(m1, VS ? hx_cur : fpv, inIxy[i]);
+        inIxz[i] = vbfi(m1, VS ? hx_cur : fpv, inIxz[i]);
+        inM[i] = vbfi(m1, VS ? hx_prev : 0u, inM[i]);
         if constexpr (LIT) {
           inIz[i] = vbfi(m1, 0u, inIz[i]);
           inIyz[i] = vbfi(m1, 0u, inIyz[i]);
           mx[i] = m1;
         }
+      }
+      if constexpr (VS) {
+        hx_prev = hx_cur;
+        hx_cur = U(H(hx_cur) + H(pa.v_lam));
       }
       lm_hi = lm_lo;
       ihi = ilo;
@@ -1041,6 +1168,8 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
       LitPre<M> lpre;
       if constexpr (LIT)
         lit_pre<M, SOP>(lit, cv, lones, a, bn, cnl, UYZ, K1, inIx, inIz, inIxy, inIyz, inIxz, inM, lpre);
+      else if constexpr (VS)
+        lap_pre_vs<M, SOP>(a, bv, c, SBC, K_, DMC, DMB, pa, inIx, inIz, inIxy, inIyz, inIxz, inM, pre);
       else if constexpr (F16)
         lap_pre_f16<M, SOP>(a, bv, c, SBC, K_, DMC, Q, pa, inIx, inIz, inIxy, inIyz, inIxz, inM, pre);
       else
@@ -1096,6 +1225,8 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
 #pragma unroll
         for (int i = 0; i < M; ++i) Ry[i] = vbfi(mx[i], 0u, Ry[i]);
         lit_post<M>(lit, Ry, UYZ, lpre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
+      } else if constexpr (VS) {
+        lap_post_vs<M>(pa, Ry, pre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
       } else if constexpr (F16) {
         lap_post_f16<M>(pa, Ry, pre, nIx, oIy, oIz, oIxy, oIyz, oIxz, oBest);
       } else {
@@ -1289,8 +1420,10 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
     // a timed-out hand-off anywhere upstream invalidates the score (every
     // workgroup of the triple precedes this one): report it in-band
     const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, SCOPE) == epoch;
+    // VS: the final cell's value sits lam (la + lb + lc) above its score
+    const int32_t vsh = VS ? pa.lam * (la + lb + lc) : 0;
     scores[tri] = bad ? TSA_SCORE_INVALID
-                      : F16 ? (int32_t)(float)__builtin_bit_cast(_Float16, hb) : (int32_t)(int16_t)hb;
+                      : F16 ? (int32_t)(float)__builtin_bit_cast(_Float16, hb) - vsh : (int32_t)(int16_t)hb;
   }
   };
   KargPtr *kout = (KargPtr *)__builtin_amdgcn_kernarg_segment_ptr();
@@ -1667,7 +1800,11 @@ static int launch_lap(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
                       const LapGeom &g, int32_t *d_scores, void *d_ws, const PencilArgs &pa,
                       hipStream_t stream, const CheckLimits *chk) {
   if (chk && F16) return TSA_EINVAL;
-  auto kfn = chk ? lap_kernel<M, NW, F16, SOP, !F16> : lap_kernel<M, NW, F16, SOP, false>;
+  // pa.lam != 0: the V-space cell (make_args(..., vs = true); f16 only)
+  LapKernelFn kfn = chk ? lap_kernel<M, NW, F16, SOP, !F16> : lap_kernel<M, NW, F16, SOP, false>;
+  if constexpr (F16) {
+    if (pa.lam != 0) kfn = lap_kernel<M, NW, true, SOP, false, false, false, true>;
+  }
   return for_each_chunk(g, n, F16, SOP, false, [&](const LapGeom &gc, int32_t c0, int32_t cn) {
     return launch_lap_fn(kfn, NW, d_seqs, d_offsets + 3 * (int64_t)c0, cn, gc, g, d_scores + c0, d_ws, pa,
                          LitArgs{}, nullptr, stream, chk);

@@ -841,6 +841,19 @@ static bool use_vs(const KParams &kp, const Range &r, int32_t max_la, int32_t ma
   return r.lo - slack >= -2048 && hi <= 2048 && (int64_t)GO + GE + kp.mismatch <= 2048;
 }
 
+// The lap kernel's V-space cell (lap_kernel VS) under the same conditions as
+// the helix's, for any tile width: lam = GE = -MISMATCH and the shifted
+// values exact f16 integers.
+static bool lap_vs_ok(const KParams &kp, const Range &r, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  if (const char *e = getenv("TSA_PENCIL_ARITH"))
+    if (!strcmp(e, "i16") || !strcmp(e, "f16")) return false;
+  const int32_t GE = kp.pen[SIXY][SIX], GO = kp.pen[SIXY][SM];
+  if (!use_f16(kp, r) || GE < 1 || GE != -kp.mismatch || GO < GE) return false;
+  const int64_t slack = pencil_slack(kp.match, kp.mismatch, GO, GE);
+  const int64_t hi = r.hi + (int64_t)GE * ((int64_t)max_la + max_lb + max_lc) + slack;
+  return r.lo - slack >= -2048 && hi <= 2048 && (int64_t)GO + GE + kp.mismatch <= 2048;
+}
+
 template <int M, int NW, bool F16, bool SOP>
 static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
                     int32_t max_lb, const PencilGeom &g, int32_t *d_scores, void *d_ws,
@@ -871,6 +884,7 @@ void pencil_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, 
   const char *s3 = kp.s3_mode == TSA_S3_SOP ? "sop" : "rtl";
   const LapGeom lg = lap_choice(n, max_la, max_lb, max_lc, lap, f16, kp.s3_mode == TSA_S3_SOP, checked);
   if (lg.ok) {
+    if (f16 && lap_vs_ok(kp, bound, max_la, max_lb, max_lc)) arith = "f16v";  // the lap's V-space cell
     char chunk[32] = "";
     if (lg.chunk > 0) snprintf(chunk, sizeof chunk, " chunk=%d", lg.chunk);
     snprintf(buf, len, "pencil lap %s %s M=%d NW=%d laps=%d tiles=%d waves=%lld%s%s est=%.0fus", arith, s3, lg.M,
@@ -896,7 +910,8 @@ int pencil_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t
   const LapGeom lg = lap_choice(n, max_la, max_lb, max_lc, lap, f16, sop, chk != nullptr);
   if (lg.ok) {
     if (ws_bytes < lap_workspace_bytes(lg)) return TSA_ENOMEM;
-    return lap_launch(lg, f16, sop, d_seqs, d_offsets, n, d_scores, d_ws, make_args(kp, f16, false), stream,
+    const bool lvs = f16 && lap_vs_ok(kp, bound, max_la, max_lb, max_lc);
+    return lap_launch(lg, f16, sop, d_seqs, d_offsets, n, d_scores, d_ws, make_args(kp, f16, lvs), stream,
                       d_err, chk);
   }
   const PencilArgs pa = make_args(kp, f16, !chk && use_vs(kp, bound, max_la, max_lb, max_lc));

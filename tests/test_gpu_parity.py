@@ -234,6 +234,34 @@ def test_vspace_helix(gpu, orc, monkeypatch, s3_mode):
         assert gpu.score_batch([(a, b, c)] * 3, p)[0] == orc.score(a, b, c)
 
 
+@pytest.mark.parametrize("geom", [(1, 4), (1, 8), (2, 4), (2, 8), (4, 8)])
+@pytest.mark.parametrize("s3_mode", [0, 1])
+def test_vspace_lap(gpu, orc, monkeypatch, geom, s3_mode):
+    """The lap kernel's V-space cell (lap_kernel VS; tools/lap_emu.py vs=True
+    replays it on the CPU): the x = 0 face injected as lam q at x = 1, lap 0's
+    y = 0 and tile 0's z = 0 face records written by the loader, the score
+    shifted back -- random, related, homopolymer and all-distinct cubes over
+    every lap geometry, laps and tiles ragged, against the oracle."""
+    m, nw = geom
+    monkeypatch.setenv("TSA_PENCIL_MODE", "lap")
+    monkeypatch.setenv("TSA_LAP_M", str(m))
+    monkeypatch.setenv("TSA_LAP_NW", str(nw))
+    rng = np.random.default_rng(300 + 10 * m + nw + s3_mode)
+    cubes = []
+    for la, lb, lc in [(70, 41, 140), (9, 33, 300), (128, 17, 64), (33, 80, 200)]:
+        cubes.append(tuple(rng.integers(0, 4, n).astype(np.uint8) for n in (la, lb, lc)))
+    base = rng.integers(0, 4, 150).astype(np.uint8)
+    rel = (base[:150].copy(), base[:120].copy(), base[:140].copy())
+    rel[1][::7] = (rel[1][::7] + 1) & 3
+    cubes += [rel, (np.zeros(90, np.uint8),) * 3, tuple(np.full(n, v, np.uint8) for n, v in ((80, 0), (66, 1), (130, 2)))]
+    for kw in [dict(), dict(gap_open=3), dict(match=0)]:
+        kw = dict(kw, s3_mode=s3_mode)
+        p, op = gpu.TsaParams.default(**kw), orc.default_params(**kw)
+        for a, b, c in cubes:
+            assert " f16v " in gpu.describe_plan(1, len(a), len(b), len(c), p, sync=False), kw
+            assert gpu.score(a, b, c, p, kernel="pencil") == orc.score(a, b, c, op), (geom, kw, len(a), len(b), len(c))
+
+
 @pytest.mark.parametrize("arith", ["f16v", "f16", "i16"])
 @pytest.mark.parametrize("s3_mode", [0, 1])
 def test_pencil_arithmetic_forms(gpu, orc, monkeypatch, arith, s3_mode):

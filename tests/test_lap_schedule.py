@@ -36,6 +36,52 @@ def test_lap_schedule_vs_oracle(orc, shape, nw, m, kind, sk):
     assert emulate(a, b, c, sop=sop, NW=nw, M=m, SK=sk) == orc.score(a, b, c, op)
 
 
+@pytest.mark.parametrize("shape,nw,m", CASES)
+@pytest.mark.parametrize("kind", ["random", "mismatch", "match", "related"])
+def test_lap_schedule_vspace_vs_oracle(orc, shape, nw, m, kind):
+    """The V-space lap (lap_kernel VS, the f16 cell of the RTL constants):
+    values shifted by lam (x+y+z), the x = 0 face injected as lam q at x = 1,
+    lap 0's y = 0 and tile 0's z = 0 records written as lam q face values --
+    the same score as the oracle over laps, tiles, NW and M (the homopolymer
+    and related cubes exercise every face)."""
+    la, lb, lc = shape
+    rng = np.random.default_rng(la * 5 + lb * 11 + lc)
+    if kind == "random":
+        a, b, c = (rng.integers(0, 4, n).astype(np.uint8) for n in shape)
+    elif kind == "mismatch":
+        a, b, c = (np.full(n, v, np.uint8) for n, v in zip(shape, (0, 1, 2)))
+    elif kind == "match":
+        a, b, c = (np.zeros(n, np.uint8) for n in shape)
+    else:
+        base = rng.integers(0, 4, max(shape)).astype(np.uint8)
+        a, b, c = (base[:n].copy() for n in shape)
+        b[::5] = (b[::5] + 1) & 3
+    sop = bool(rng.integers(0, 2))
+    op = orc.default_params(score_bits=16, s3_mode=int(sop))
+    assert emulate(a, b, c, sop=sop, NW=nw, M=m, vs=True) == orc.score(a, b, c, op)
+
+
+def test_lap_vspace_split_cell_algebra():
+    """csrc/lap_kernel.hip:lap_pre_vs / lap_post_vs (the V-space cell split at
+    the row above) equal cell_messages_vs (pencil_common.h) for any inputs,
+    GO >= GE and lam = GE = -MISMATCH (DO = GO - GE >= 0, CP = GO >= lam)."""
+    from lap_emu import vs_cell
+    rng = np.random.default_rng(11)
+    for _ in range(20000):
+        lam = int(rng.integers(1, 5))
+        go = int(rng.integers(lam, 9))
+        cP, dO = go - lam + lam, go - lam
+        X, Y, Z, XY, XZ, YZ, Mv = (int(v) for v in rng.integers(-40, 40, 7))
+        Gx, Gy, Gz = max(Y, Z, YZ), max(X, Z, XZ), max(X, Y, XY)
+        best = max(Gx, Gy, XY, Mv)
+        b1 = best - dO
+        pxy, pyz, pxz = max(Gz, b1), max(Gx, b1), max(Gy, b1)
+        qxy, qyz, qxz = pxy - cP, pyz - cP, pxz - cP
+        ref = (best, max(X - lam, qxy, qxz), max(Y - lam, qxy, qyz), max(Z - lam, qyz, qxz), pxy, pyz, pxz)
+        got = tuple(int(v) for v in vs_cell(*(np.int64(v) for v in (X, Y, Z, XY, YZ, XZ, Mv)), lam, cP, dO))
+        assert got == ref
+
+
 def test_lap_split_cell_algebra():
     """csrc/lap_kernel.hip:lap_pre_*/lap_post_* fold every message to
     max(Y - c, N) with the N's independent of the row above (Y = Iy's input);

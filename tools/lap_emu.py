@@ -47,9 +47,29 @@ def codes(seq, n):
     return out
 
 
-def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, SK=1, cells=None):
+def vs_cell(X, Y, Z, XY, YZ, XZ, Mv, lam, cP, dO):
+    """lap_kernel.hip's V-space cell split at the row above (lap_pre_vs before
+    Y lands, lap_post_vs after): inputs with their pair / triple scores added,
+    returns (best, Ix', Iy', Iz', Ixy', Iyz', Ixz')."""
+    gx, gz, Gy = np.maximum(Z, YZ), np.maximum(X, XY), np.maximum(np.maximum(X, Z), XZ)
+    W = np.maximum(np.maximum(gx, Gy), np.maximum(XY, Mv))
+    WD = W - dO
+    NXY, NYZ, NXZ = np.maximum(gz, WD), np.maximum(gx, WD), np.maximum(Gy, WD)
+    N1 = np.maximum(np.maximum(X - lam, NXY - cP), NXZ - cP)
+    N2 = np.maximum(NXY - cP, NYZ - cP)
+    N3 = np.maximum(np.maximum(Z - lam, NYZ - cP), NXZ - cP)
+    return (np.maximum(Y, W), np.maximum(Y - cP, N1), np.maximum(Y - lam, N2), np.maximum(Y - cP, N3),
+            np.maximum(Y, NXY), np.maximum(Y, NYZ), np.maximum(Y - dO, NXZ))
+
+
+def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, SK=1, cells=None, vs=False):
     """Score of one triple by the lap schedule (no wrap: valid where the
-    factored form is exact)."""
+    factored form is exact). vs: the V-space cell (lap_kernel VS: values
+    shifted by lam (x+y+z), lam = GE = -MISMATCH) with its face values --
+    x = 1 injection, lap 0's y = 0 records, tile 0's z = 0 records."""
+    lam = ge if vs else 0
+    assert not vs or ge == -mismatch
+    cP, dO, dm = go + mismatch + lam, go - ge, match - mismatch
     la, lb, lc = len(a), len(b), len(c)
     P = penalties(go, ge)
     RW, ZT = 2 * NW, 64 * M
@@ -94,6 +114,15 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, SK=
             svM = np.zeros((2,) + shape, np.int64)
             own_prev = np.zeros((4,) + shape, np.int64)
             out_prev = np.zeros((4,) + shape, np.int64)    # wave w's record of step t-1
+            if q == 0 and vs:  # tile 0: the face records of steps -1 and -2 (zface_vs)
+                for w in range(NW):
+                    for tt, ph in ((-1, 1), (-2, 0)):
+                        g1, g2 = lam * (tt + L * RW + 2), lam * (tt + L * RW + 3)
+                        if tt == -1:
+                            shIz[w, 0, 0] = g1
+                            svIyz[w, 0, 0] = g1
+                        shIxz[ph, w, 0, 0] = g2
+                        svM[ph, w, 0, 0] = g1
             if q > 0:
                 # position 0 before step 0: the shifts of steps -2 and -1 would have
                 # brought in the left tile's records ZT-2 and ZT-1 (Iz, Iyz feed the
@@ -126,7 +155,10 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, SK=
                     # ---- the row above
                     if w == 0:
                         if L == 0:
-                            above = np.array(face, np.int64)[:, None, None, None] * np.ones((4, M, 64, 2), np.int64)
+                            fc = face
+                            if vs:  # the loader's yface_vs(t): zoff = q ZT
+                                fc = (lam * (t + q * ZT + 1),) + (lam * (t + q * ZT + 2),) * 3
+                            above = np.array(fc, np.int64)[:, None, None, None] * np.ones((4, M, 64, 2), np.int64)
                         else:
                             prev = yrec[(L - 1, q)]
                             r = t + YOFF
@@ -146,10 +178,14 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, SK=
                     # ---- x = 1 injection (u == 0)
                     u = np.stack([ulo, ulo - 1], -1) * np.ones((M, 64, 2), np.int64)
                     inj = u == 0
-                    inIx[inj] = f_single
-                    inIxy[inj] = f_pair
-                    inIxz[inj] = f_pair
-                    inM[inj] = 0
+                    if vs:  # lam (t + L RW + zoff + 1) for both halves; M one lam less
+                        hx = lam * (t + L * RW + q * ZT + 1)
+                        inIx[inj], inIxy[inj], inIxz[inj], inM[inj] = hx, hx, hx, hx - lam
+                    else:
+                        inIx[inj] = f_single
+                        inIxy[inj] = f_pair
+                        inIxz[inj] = f_pair
+                        inM[inj] = 0
                     # ---- scores (one-hot codes; 0 = padding never matches)
                     eab = (acode & bcode) != 0
                     eac = (acode & ccode) != 0
@@ -159,9 +195,17 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, SK=
                         s3 = s2(eab) + s2(ebc) + s2(eac)
                     else:
                         s3 = np.where(eab, np.where(ebc, s3_eq, s3_ab), s3_ne)
-                    S = np.stack([inM + s3, inIx, inIy, inIz, inIxy + s2(eab), inIyz + s2(ebc),
-                                  inIxz + s2(eac)])
-                    msg = np.stack([(S - P[T_][:, None, None, None]).max(0) for T_ in range(7)])
+                    if vs:  # the kernel's V-space inputs: pair scores as dm [match], M's + 3 lam = 0 (RTL)
+                        if sop:
+                            Mv = inM + s3 + 3 * lam
+                        else:
+                            Mv = inM + np.where(eab, np.where(ebc, s3_eq, s3_ab) - s3_ne, 0) + s3_ne + 3 * lam
+                        S = np.stack([Mv, inIx, inIy, inIz, inIxy + dm * eab, inIyz + dm * ebc, inIxz + dm * eac])
+                        msg = np.stack(vs_cell(inIx, inIy, inIz, S[4], S[5], S[6], Mv, lam, cP, dO))
+                    else:
+                        S = np.stack([inM + s3, inIx, inIy, inIz, inIxy + s2(eab), inIyz + s2(ebc),
+                                      inIxz + s2(eac)])
+                        msg = np.stack([(S - P[T_][:, None, None, None]).max(0) for T_ in range(7)])
                     if cells is not None:  # debugging: the 7 states of every real cell
                         for i in range(M):
                             for l in range(64):
@@ -179,7 +223,7 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, SK=
                         rf = (lb - 1) - L * RW
                         kf = (lc - 1) - q * ZT
                         if rf // 2 == w and t == (la - 1) + tau(rf) + kf:
-                            score = int(best[kf % M, kf // M, rf % 2])
+                            score = int(best[kf % M, kf // M, rf % 2]) - lam * (la + lb + lc)
                     # ---- z staging: lane 63, register M-1
                     zstep[w] = (oIz[M - 1, 63].copy(), oIxz[M - 1, 63].copy(),
                                 REC[2][M - 1, 63].copy(), REC[3][M - 1, 63].copy())
@@ -190,6 +234,9 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, NW=2, M=1, SK=
                         left = zrec[(L, q - 1)]
                         rz = t + ZT
                         fz = left[min(rz, len(left) - 1)][w]
+                    elif vs:  # the loader's zface_vs(t + ZT)
+                        g1, g2 = lam * (t + L * RW + 2), lam * (t + L * RW + 3)
+                        fz = (np.array([g1] * 2), np.array([g2] * 2), np.array([g1] * 2), np.array([g1] * 2))
                     else:
                         fz = (np.array([f_single] * 2), np.array([f_pair] * 2),
                               np.array([f_pair] * 2), np.array([0, 0]))
