@@ -540,6 +540,7 @@ def single_specs(args, L):
 
 
 DAT_KEY = "configs[0]: dat/{A,B,C}_seq.dat"
+SPIN_OK = [True]  # torch.cuda._sleep usable as the single cubes' preload
 
 
 def dat_triple():
@@ -573,16 +574,27 @@ def time_singles(args, tsa, synth, hot, dev, L, params, reps=None):
         sstep()
         torch.cuda.synchronize()
 
+        def spin():
+            if SPIN_OK[0]:
+                try:
+                    torch.cuda._sleep(2_000_000)  # ~1 ms of clock spinning, no memory traffic
+                    return
+                except Exception:  # noqa: BLE001  (no such op on this build: the batch instead)
+                    SPIN_OK[0] = False
+            hot.step()
+
         def timed(preload):
-            # preload: the batch launch queued first keeps the GPU busy while
-            # the host submits e0, the cube's launch(es) and e1, so e0 -> e1 is
-            # the device time of the call; without it the span also holds the
-            # host's submission latency (the round-3 figure)
+            # preload: a spin kernel queued first keeps the GPU busy while the
+            # host submits e0, the cube's launch(es) and e1, so e0 -> e1 is the
+            # device time of the call; without it the span also holds the
+            # host's submission latency (the round-3 figure). The spin touches
+            # no memory (a batch launch as the preload left dirty L2 lines that
+            # slowed the cube after it)
             times = []
             for _ in range(reps or nrep):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 if preload:
-                    hot.step()
+                    spin()
                 e0.record(stream)
                 sstep()
                 e1.record(stream)
@@ -594,7 +606,7 @@ def time_singles(args, tsa, synth, hot, dev, L, params, reps=None):
              "score": int(s_score.item()), "score_bits": prm.score_bits,
              "plan": tsa.describe_plan(1, la, lb, lc, prm, kernel=kernel, sync=False),
              "timing": "device: median of HIP events around the call's launches, queued behind a "
-                       "batch launch so host submission is hidden" if hot.n > 0 else "events, host submit included"}
+                       "spin kernel so host submission is hidden" if hot.n > 0 else "events, host submit included"}
         if hot.n > 0:
             r["ms_incl_submit"] = round(timed(preload=False), 4)
         if Ls in ASIC_MS and prm.score_bits == 12 and trip is None:

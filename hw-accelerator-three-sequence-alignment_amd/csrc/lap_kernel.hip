@@ -1552,9 +1552,13 @@ static int lap_blocks_per_cu_lit(size_t lds) {
 // chain steps include the hand-off stalls.
 // LIT: the literal cell's step, ~1.6x the message form's (single cubes and
 // batches, profiles/r3l_literal_lap_vs_plane.jsonl, r3o_chunk.jsonl).
+// M = 1 with two workgroups per CU (the latency-bound waves share SIMDs):
+// ~0.97 us per chained step (16 x 256^3 and 1024^3 in rounds,
+// profiles/r4c_lapab.jsonl), twice the one-per-CU step.
 static double lap_step_us(int M, int NW, int64_t wg_per_cu, bool lit = false) {
   const double base = M == 1 ? (NW == 4 ? 0.40 : 0.49) : M == 2 ? 0.62 : 1.45;
-  return (lit ? 1.6 : 1.0) * base * (1.0 + 0.22 * (double)(std::max<int64_t>(wg_per_cu, 1) - 1));
+  const double share = M == 1 ? 1.0 : 0.22;  // per extra workgroup on the CU
+  return (lit ? 1.6 : 1.0) * base * (1.0 + share * (double)(std::max<int64_t>(wg_per_cu, 1) - 1));
 }
 
 LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int M, int NW,

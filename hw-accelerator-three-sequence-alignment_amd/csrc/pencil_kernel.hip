@@ -844,7 +844,14 @@ static bool use_vs(const KParams &kp, const Range &r, int32_t max_la, int32_t ma
 // The lap kernel's V-space cell (lap_kernel VS) under the same conditions as
 // the helix's, for any tile width: lam = GE = -MISMATCH and the shifted
 // values exact f16 integers.
+// Opt-in (TSA_LAP_VS=1): measured slower than the message form on MI355X
+// (64^3 0.098 vs 0.087 ms, 256^3 0.412 vs 0.389 ms, same box,
+// profiles/r4c_lapvs.jsonl) -- the chained lap step is bound by its loader's
+// hand-off, not by the cell's instructions, and the V-space faces make lap 0's
+// wave 0 wait on its loader, which the message form's constant faces do not.
 static bool lap_vs_ok(const KParams &kp, const Range &r, int32_t max_la, int32_t max_lb, int32_t max_lc) {
+  const char *on = getenv("TSA_LAP_VS");
+  if (!on || atoi(on) == 0) return false;
   if (const char *e = getenv("TSA_PENCIL_ARITH"))
     if (!strcmp(e, "i16") || !strcmp(e, "f16")) return false;
   const int32_t GE = kp.pen[SIXY][SIX], GO = kp.pen[SIXY][SM];

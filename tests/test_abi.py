@@ -100,9 +100,15 @@ def test_describe_plan(tsa):
     assert tsa.describe_plan(512, 256, 256, 256, tsa.TsaParams.default(gap_extend=2, gap_open=3)
                              ).startswith("pencil helix f16 rtl")
     assert tsa.describe_plan(512, 400, 400, 400, p).startswith("pencil helix f16 rtl M=4")
-    # a single cube: the lap kernel, in V-space (f16v) while the shifted values stay exact f16
-    assert tsa.describe_plan(1, 256, 256, 256, p).startswith("pencil lap f16v rtl M=1")
-    assert tsa.describe_plan(1, 512, 512, 512, p).startswith("pencil lap f16 rtl M=1")
+    # a single cube: the lap kernel (its V-space cell only on request, TSA_LAP_VS=1)
+    assert tsa.describe_plan(1, 256, 256, 256, p).startswith("pencil lap f16 rtl M=1")
+    import os
+    os.environ["TSA_LAP_VS"] = "1"
+    try:
+        assert tsa.describe_plan(1, 256, 256, 256, p).startswith("pencil lap f16v rtl M=1")
+        assert tsa.describe_plan(1, 512, 512, 512, p).startswith("pencil lap f16 rtl M=1")  # beyond exact f16
+    finally:
+        del os.environ["TSA_LAP_VS"]
     # a few cubes: the lap kernel; many: the helix; a batch beyond the lap
     # grid's dispatch-round rules runs as chunks of triples, one launch each
     assert tsa.describe_plan(4, 256, 256, 256, p, sync=False).startswith("pencil lap f16")

@@ -243,6 +243,7 @@ def test_vspace_lap(gpu, orc, monkeypatch, geom, s3_mode):
     shifted back -- random, related, homopolymer and all-distinct cubes over
     every lap geometry, laps and tiles ragged, against the oracle."""
     m, nw = geom
+    monkeypatch.setenv("TSA_LAP_VS", "1")  # opt-in (slower than the message form on MI355X)
     monkeypatch.setenv("TSA_PENCIL_MODE", "lap")
     monkeypatch.setenv("TSA_LAP_M", str(m))
     monkeypatch.setenv("TSA_LAP_NW", str(nw))

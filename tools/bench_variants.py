@@ -68,9 +68,11 @@ def main():
     for _ in range(args.rounds):
         for v in args.variants:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            if pre is not None:
-                apply(v)  # (the knobs first: run() re-applies them after the preload is queued)
-                torch.mm(pre, pre)
+            if pre is not None:  # a spin (no memory traffic), else a matmul
+                if hasattr(torch.cuda, "_sleep"):
+                    torch.cuda._sleep(2_000_000)
+                else:
+                    torch.mm(pre, pre)
             e0.record(st)
             run(v)
             e1.record(st)
