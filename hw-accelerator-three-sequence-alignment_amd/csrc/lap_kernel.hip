@@ -471,8 +471,11 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 #ifndef TSA_LAP_WPE2
 #define TSA_LAP_WPE2 4
 #endif
+#ifndef TSA_LAP_WPE1
+#define TSA_LAP_WPE1 6
+#endif
 __host__ __device__ constexpr int lap_waves_per_eu(int M, bool lit = false) {
-  return lit ? (M == 1 ? 6 : 3) : M == 1 ? 6 : M == 2 ? TSA_LAP_WPE2 : 2;
+  return lit ? (M == 1 ? TSA_LAP_WPE1 : 3) : M == 1 ? TSA_LAP_WPE1 : M == 2 ? TSA_LAP_WPE2 : 2;
 }
 // f(integral_constant<J>) for J = B .. E-1, unrolled at compile time
 template <int B, int E, class F>
