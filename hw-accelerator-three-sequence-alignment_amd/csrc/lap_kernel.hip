@@ -471,6 +471,9 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 #ifndef TSA_LAP_WPE2
 #define TSA_LAP_WPE2 4
 #endif
+#ifndef TSA_LAP_LAUNDER
+#define TSA_LAP_LAUNDER 1
+#endif
 #ifndef TSA_LAP_WPE1
 #define TSA_LAP_WPE1 6
 #endif
@@ -509,9 +512,11 @@ __device__ __forceinline__ void static_for(F &&f) {
 // step) into the rings wave 0 and position 0 read, values are shifted left by
 // 16 - SCORE_BITS so int16 adds wrap at the RTL word, and the final cell's 7
 // input states go to mon (aux) as its final 7-tuple.
-// The kernel's arguments, one by-value struct: the round loop reads them
-// through a pointer laundered per lap, so no argument is held in registers
-// across the loop (each lap reloads what it uses, as one pass would).
+// The kernel's arguments, bundled on the host and passed as separate
+// __restrict__ parameters (LAP_KARGS). Measured: one by-value struct read
+// through the kernarg segment pointer ran single cubes 15 % slower (64^3 0.087
+// vs 0.075 ms, 256^3 0.40 vs 0.355 ms, same box, profiles/r4i_single_ab.jsonl)
+// -- likely the no-alias guarantee the parameters carry and the fields do not.
 struct LapKArgs {
   const uint8_t *seqs;
   const int64_t *offs;
@@ -529,23 +534,21 @@ struct LapKArgs {
   unsigned long long *trace;
   LitArgs lit;
 };
-// A kernarg-segment struct, word by word (scalar loads into registers)
-template <class T>
-__device__ __forceinline__ T kload(const __attribute__((address_space(4))) T &src) {
-  static_assert(sizeof(T) % 4 == 0, "word-sized");
-  T r;
-  uint32_t *d = (uint32_t *)&r;
-  const __attribute__((address_space(4))) uint32_t *w = (const __attribute__((address_space(4))) uint32_t *)&src;
-#pragma unroll
-  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) d[i] = w[i];
-  return r;
-}
+#define LAP_KARGS(k)                                                                                   \
+  k.seqs, k.offs, k.G, k.GZ, k.NC, k.CH, k.YR, k.ZR, k.yf_base, k.zf_base, k.rd, k.prog, k.err, k.scores, \
+      k.mon, k.pa, k.epoch, k.spin_limit, k.L0, k.L1, k.yf_out, k.prog_in, k.trace, k.lit
 // VS: the V-space f16 cell (lap_pre_vs), every value shifted by lam (x+y+z):
 // the faces become lam q (the x = 0 face injected at x = 1, the y = 0 / z = 0
 // faces written by the loader like the literal form's), the score shifted
 // back at the end.
 template <int M, int NW, bool F16, bool SOP, bool CHK, bool SYS = false, bool LIT = false, bool VS = false>
-__global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_kernel(const LapKArgs ka) {
+__global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_kernel(
+    const uint8_t *__restrict__ seqs_, const int64_t *__restrict__ offs_, int32_t G_, int32_t GZ_,
+    int32_t NC_, int32_t CH_, int32_t YR_, int32_t ZR_, uint8_t *__restrict__ yf_base_,
+    uint8_t *__restrict__ zf_base_, LapRounds rd_, int32_t *__restrict__ prog_, uint32_t *__restrict__ err_,
+    int32_t *__restrict__ scores_, int32_t *__restrict__ mon_, PencilArgs pa_, uint32_t epoch_,
+    uint32_t spin_limit_, int32_t L0_, int32_t L1_, uint8_t *__restrict__ yf_out_,
+    int32_t *__restrict__ prog_in_, unsigned long long *__restrict__ trace_, LitArgs lit_) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   static_assert(!(CHK && F16), "the checked kernel runs the int16 form");
   static_assert(!(CHK && SYS), "a split cube runs the unchecked forms");
@@ -581,34 +584,30 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
   // slots p/8, p/8 + SX, p/8 + 2 SX, ... of its XCD one after another -- lap
   // order per physical workgroup whatever the dispatcher does, and a slot's
   // next lap starts the moment its previous one ends. One round: one pass.
-  typedef const __attribute__((address_space(4))) LapKArgs KargPtr;  // the kernarg segment (scalar loads)
   auto lap_body = [&](const int32_t slot) {
-  // ka sits at offset 0 of the kernarg segment (its only explicit argument);
-  // taking &ka would copy it to private memory and make every field divergent
-  KargPtr *kap = (KargPtr *)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(kap));
-  KargPtr &A = *kap;
-  const uint8_t *__restrict__ seqs = A.seqs;
-  const int64_t *__restrict__ offs = A.offs;
-  const int32_t G = A.G, GZ = A.GZ, NC = A.NC, CH = A.CH, YR = A.YR, ZR = A.ZR;
-  uint8_t *__restrict__ yf_base = A.yf_base, *__restrict__ zf_base = A.zf_base;
-  const LapRounds rd = kload(A.rd);
-  int32_t *__restrict__ prog = A.prog;
-  uint32_t *__restrict__ err = A.err;
-  int32_t *__restrict__ scores = A.scores, *__restrict__ mon = A.mon;
-  const PencilArgs pa = kload(A.pa);
-  const uint32_t epoch = A.epoch, spin_limit = A.spin_limit;
-  const int32_t L0 = A.L0, L1 = A.L1;
-  uint8_t *__restrict__ yf_out = A.yf_out;
-  int32_t *__restrict__ prog_in = A.prog_in;
-  unsigned long long *__restrict__ trace = A.trace;
-  const LitArgs lit = kload(A.lit);
+  const uint8_t *__restrict__ seqs = seqs_;
+  const int64_t *__restrict__ offs = offs_;
+  const int32_t G = G_, GZ = GZ_, NC = NC_, CH = CH_, YR = YR_, ZR = ZR_;
+  uint8_t *__restrict__ yf_base = yf_base_, *__restrict__ zf_base = zf_base_;
+  const LapRounds &rd = rd_;
+  int32_t *__restrict__ prog = prog_;
+  uint32_t *__restrict__ err = err_;
+  int32_t *__restrict__ scores = scores_, *__restrict__ mon = mon_;
+  const PencilArgs &pa = pa_;
+  const uint32_t epoch = epoch_, spin_limit = spin_limit_;
+  const int32_t L0 = L0_, L1 = L1_;
+  uint8_t *__restrict__ yf_out = yf_out_;
+  int32_t *__restrict__ prog_in = prog_in_;
+  unsigned long long *__restrict__ trace = trace_;
+  const LitArgs &lit = lit_;
   const int32_t b = 8 * slot + (int32_t)(blockIdx.x & 7);  // logical block
   // the lane / thread index laundered per lap: otherwise the compiler hoists
   // every per-lane address out of the round loop and keeps it live across
   // the whole body (+20 VGPRs, measured), where one pass rematerialises them
   int32_t tid = (int32_t)threadIdx.x;
+#if TSA_LAP_LAUNDER
   asm volatile("" : "+v"(tid));
+#endif
   const int lane = tid & 63;
   const int32_t L = L0 + slot / CH, col = (slot % CH) * 8 + (b & 7);
   if (col >= NC || L >= L1) return;  // padding block
@@ -1429,8 +1428,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_k
                       : F16 ? (int32_t)(float)__builtin_bit_cast(_Float16, hb) - vsh : (int32_t)(int16_t)hb;
   }
   };
-  KargPtr *kout = (KargPtr *)__builtin_amdgcn_kernarg_segment_ptr();
-  const int32_t slots = (kout->L1 - kout->L0) * kout->CH, sx = kout->rd.SX;  // logical slots per XCD
+  const int32_t slots = (L1_ - L0_) * CH_, sx = rd_.SX;  // logical slots per XCD
   for (int32_t slot = (int32_t)(blockIdx.x >> 3); slot < slots; slot += sx) {
     lap_body(slot);
     __syncthreads();  // the next lap re-initialises this workgroup's LDS
@@ -1753,7 +1751,7 @@ static int launch_lap_fn(LapKernelFn kfn, int NW, const uint8_t *d_seqs, const i
   const uint32_t epoch = lap_next_epoch();
   const LapKArgs ka{d_seqs, d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, rd, prog, err,
                     d_scores, mon, pa, epoch, lap_spin_limit(), 0, g.G, yf, prog, trace, lit};
-  hipLaunchKernelGGL(kfn, dim3((uint32_t)g.grid), dim3(64 * (NW + 1)), g.lds, stream, ka);
+  hipLaunchKernelGGL(kfn, dim3((uint32_t)g.grid), dim3(64 * (NW + 1)), g.lds, stream, LAP_KARGS(ka));
   if (chk) {
     if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
     hipLaunchKernelGGL(lap_certify, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, mon, n,
@@ -1879,7 +1877,7 @@ static int launch_split_fn(LapKernelFn kfn, int NW, const LapGeom &g, const Penc
     const LapKArgs ka{q.d_seqs, q.d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, lap_rounds(g, q.d_ws),
                       prog, d_err, d_score, (int32_t *)nullptr, pa, epoch, spin, q.L0, q.L1, yf_out, prog_in,
                       (unsigned long long *)nullptr, lit};
-    hipLaunchKernelGGL(kfn, dim3((uint32_t)blocks), dim3(64 * (NW + 1)), g.lds, q.stream, ka);
+    hipLaunchKernelGGL(kfn, dim3((uint32_t)blocks), dim3(64 * (NW + 1)), g.lds, q.stream, LAP_KARGS(ka));
     if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
   }
   return TSA_OK;

@@ -87,10 +87,17 @@ def main():
         trip = [synth.triple(i, L) for i in idx]
         cs, co = tsa.pack_batch(trip)
         ref = oracle.score_batch(cs, co, oracle.default_params(score_bits=args.score_bits), nthreads=8)
+    plans = {}
+    for v in args.variants:
+        apply(v)
+        try:
+            plans[v] = tsa.describe_plan(n, L, L, L, p, args.kernel, sync=False)
+        except Exception as e:  # noqa: BLE001 -- a label only
+            plans[v] = f"? ({e})"
     for v in args.variants:
         med = statistics.median(times[v])
         rec = {"variant": v, "n": n, "L": L, "median_ms": round(med, 4), "min_ms": round(min(times[v]), 4),
-               "gcups": round(n * L ** 3 / (med * 1e-3) / 1e9, 2)}
+               "gcups": round(n * L ** 3 / (med * 1e-3) / 1e9, 2), "plan": plans[v]}
         if ref is not None:
             rec["parity_ok"] = bool((scores[v][idx] == ref).all())
         # every variant must score the batch identically (and never the
