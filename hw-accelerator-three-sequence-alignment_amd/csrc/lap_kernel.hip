@@ -467,7 +467,13 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 // balance them), so two NW = 8 workgroups per CU need 6 waves per SIMD, i.e.
 // <= 80 VGPRs: with 96 (5 waves) the CU admitted one, and the second half of
 // a 1024^3 lap grid started only as the first half finished (ring-lag census,
-// profiles/r3e_lap_lag.jsonl). M = 1 fits 6 as it is; M >= 4 runs one per CU.
+// profiles/r3e_lap_lag.jsonl). M = 1 keeps 6 for the plain forms (the int16
+// one needs the cap to stay two per CU, tests/test_kernel_meta.py) and asks
+// for 4 for the checked and literal ones, which spill 8 bytes at 6; the f16
+// single cubes stay <= 80 VGPRs either way and ran alike (same box: 64^3
+// 0.0741 ms at 4 vs 0.0748 at 6, 256^3 0.351 vs 0.356; without the per-lap
+// index launder (TSA_LAP_LAUNDER=0) 256^3 0.366, profiles/r4j_single_ab.jsonl).
+// M >= 4 runs one per CU.
 #ifndef TSA_LAP_WPE2
 #define TSA_LAP_WPE2 4
 #endif
@@ -477,8 +483,8 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 #ifndef TSA_LAP_WPE1
 #define TSA_LAP_WPE1 6
 #endif
-__host__ __device__ constexpr int lap_waves_per_eu(int M, bool lit = false) {
-  return lit ? (M == 1 ? TSA_LAP_WPE1 : 3) : M == 1 ? TSA_LAP_WPE1 : M == 2 ? TSA_LAP_WPE2 : 2;
+__host__ __device__ constexpr int lap_waves_per_eu(int M, bool lit = false, bool chk = false) {
+  return lit ? (M == 1 ? 4 : 3) : M == 1 ? (chk ? 4 : TSA_LAP_WPE1) : M == 2 ? TSA_LAP_WPE2 : 2;
 }
 // f(integral_constant<J>) for J = B .. E-1, unrolled at compile time
 template <int B, int E, class F>
@@ -542,7 +548,7 @@ struct LapKArgs {
 // faces written by the loader like the literal form's), the score shifted
 // back at the end.
 template <int M, int NW, bool F16, bool SOP, bool CHK, bool SYS = false, bool LIT = false, bool VS = false>
-__global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT)) void lap_kernel(
+__global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void lap_kernel(
     const uint8_t *__restrict__ seqs_, const int64_t *__restrict__ offs_, int32_t G_, int32_t GZ_,
     int32_t NC_, int32_t CH_, int32_t YR_, int32_t ZR_, uint8_t *__restrict__ yf_base_,
     uint8_t *__restrict__ zf_base_, LapRounds rd_, int32_t *__restrict__ prog_, uint32_t *__restrict__ err_,
