@@ -17,6 +17,9 @@ typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 constexpr size_t LDS_MAX = 160 * 1024;
 constexpr int REC_BYTES = 16;      // {Iy, Ixy, Iyz, best} packed pairs per lane
+#ifndef TSA_A_B64  // V-space M = 2: a step's A codes as one ds_read_b64 (pencil_kernel)
+#define TSA_A_B64 1
+#endif
 #ifndef TSA_A_PREFETCH  // read the next step's A codes before the step barrier
 #define TSA_A_PREFETCH 1
 #endif
@@ -456,6 +459,22 @@ __device__ __forceinline__ void load_a_off(uint32_t va, int off, uint32_t (&a)[M
       (const __attribute__((address_space(3))) uint32_t *)(uintptr_t)va;
 #pragma unroll
   for (int i = 0; i < M; ++i) a[i] = p[off + M - 1 - i];
+}
+// V-space, M = 2: entries OFF and OFF + 1 of va's table as one ds_read_b64
+// (a[1] = entry OFF, a[0] = OFF + 1). The group's first entry va is odd, so
+// the pair is 8-byte aligned in the table itself for odd OFF, and in the copy
+// shifted by one entry (va_s: entry j holds the table's j + 1) for even OFF.
+// Lanes 8 B apart then read 512 contiguous bytes, conflict-free in both
+// 32-lane groups; ds_read2_b32 is serviced as two ds_read_b32 banked mod 32,
+// which lanes two dwords apart make 2-way (MI355X_MICROARCH.md, LDS).
+template <int OFF>
+__device__ __forceinline__ void load_a_pair(uint32_t va, uint32_t va_s, uint32_t (&a)[2]) {
+  const uint32_t addr = (OFF & 1) ? va + 4u * OFF : va_s + 4u * (OFF - 1);
+  // one 64-bit integer load (a uint2 is split into two dword loads, which the
+  // backend re-merges into ds_read2_b32 unless it can prove the alignment)
+  const uint64_t v = *(const __attribute__((address_space(3))) uint64_t *)(uintptr_t)addr;
+  a[1] = (uint32_t)v;
+  a[0] = (uint32_t)(v >> 32);
 }
 // bfi mask selecting one half (hs) of one lane (ls): the lane bit comes from a
 // scalar shift, so this is one VALU op (v_cndmask with an SGPR-pair mask);

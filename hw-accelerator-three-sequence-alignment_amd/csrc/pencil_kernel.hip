@@ -91,8 +91,10 @@ static PencilGeom pencil_geom(int32_t max_la, int32_t max_lc) {
   return g;
 }
 static size_t helix_lds(int M, int NW, int32_t P, int32_t max_lb) {
-  return (size_t)(NW - 1) * 2 * helix_skew(M) * M * 1024 + (size_t)helix_pd(M) * M * 1024 +
-         4 * ((size_t)P + 128 * M + A_PAD) + 4 * (((size_t)max_lb + 3) & ~(size_t)3) + (size_t)M * 512;
+  // M = 2 (TSA_A_B64): the A table's copy shifted by one entry after fin
+  const size_t a_tab = 4 * ((size_t)P + 128 * M + A_PAD);
+  return (size_t)(NW - 1) * 2 * helix_skew(M) * M * 1024 + (size_t)helix_pd(M) * M * 1024 + a_tab +
+         4 * (((size_t)max_lb + 3) & ~(size_t)3) + (size_t)M * 512 + (M == 2 && TSA_A_B64 ? a_tab : 0);
 }
 
 // The factored messages widen each target's highest-penalty group to all seven
@@ -226,6 +228,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
   uint32_t *sA2 = (uint32_t *)(xr0 + PD * SLOT_BYTES);
   uint32_t *sB = (uint32_t *)((uint8_t *)sA2 + lds_a);
   uint32_t *fin = (uint32_t *)((uint8_t *)sB + lds_b);
+  uint32_t *sA2s = (uint32_t *)((uint8_t *)fin + M * 512);  // A_B64: sA2 shifted by one entry
+  constexpr bool A_B64 = VS && M == 2 && TSA_A_B64;
 
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -273,11 +277,15 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 
     // ---- stage A codes (padded to P, halves k/k+64M or, TWO, the two triples) and
     // B; face records in the ring
-    for (int j = threadIdx.x; j < P + ZT + A_PAD; j += 64 * NW) {  // periodic in j: the pad repeats P
+    auto a_entry = [&](int j) -> uint32_t {  // periodic in j: the pad repeats P
       const int x0 = ((j - ZT) % P + P) % P, x1 = TWO ? x0 : ((j - ZT - 64 * M) % P + P) % P;
       const uint32_t c0 = x0 < la ? SYM0 << tsa_sym(seqs, o0 + x0, pa.packed) : 0u;
       const uint32_t c1 = x1 < la1 ? SYM0 << tsa_sym(seqs, (TWO ? q0 : o0) + x1, pa.packed) : 0u;
-      sA2[j] = c0 | (c1 << 16);
+      return c0 | (c1 << 16);
+    };
+    for (int j = threadIdx.x; j < P + ZT + A_PAD; j += 64 * NW) {
+      sA2[j] = a_entry(j);
+      if constexpr (A_B64) sA2s[j] = a_entry(j + 1);
     }
     for (int i = threadIdx.x; i < lbm; i += 64 * NW) {
       if constexpr (TWO)
@@ -414,6 +422,9 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     if constexpr (TSA_A_PREFETCH) load_a<M>(a_lane + 4u * (uint32_t)xpos0, a_nx);
     int32_t st_row = 0;                          // ring row written at step t (last wave)
     uint32_t abase = a_lane;                     // VS: A address of the group's first step
+    // A_B64: the same entry in the shifted copy
+    const uint32_t a_lane_s = a_lane + (uint32_t)((uint8_t *)sA2s - (uint8_t *)sA2);
+    uint32_t abase_s = a_lane_s;
 
     // VS: the step whose cell is the final one, in this wave (-1: none)
     const int32_t t_fin = w == w_f ? T - 1 : -1;
@@ -640,7 +651,8 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         zshift<M>(svM[PH], rw, sel, 0u);
         advance();
       }
-      if constexpr (VS) load_a_off<M>(abase, (PQ & 3) + 1, a_nx);  // x' of step t + 1
+      if constexpr (A_B64) load_a_pair<(PQ & 3) + 1>(abase, abase_s, a_nx);  // x' of step t + 1
+      else if constexpr (VS) load_a_off<M>(abase, (PQ & 3) + 1, a_nx);
       else if constexpr (TSA_A_PREFETCH) load_a<M>(a_lane + 4u * (uint32_t)xpos0, a_nx);
 
       // ---- wave 0: fetch the record of step t + PD into the slot just consumed
@@ -677,6 +689,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll 1
         for (; t < T; t += 4) {
           abase = a_lane + 4u * (uint32_t)xpos0;
+          if constexpr (A_B64) abase_s = a_lane_s + 4u * (uint32_t)xpos0;
           TSA_INLINE_IF_WIDE(step(Q0, role, t, mid));
           TSA_INLINE_IF_WIDE(step(Q1, role, t + 1, mid));
           TSA_INLINE_IF_WIDE(step(Q2, role, t + 2, mid));
