@@ -477,6 +477,9 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 #ifndef TSA_LAP_WPE2
 #define TSA_LAP_WPE2 4
 #endif
+#ifndef TSA_LAP_WPE2C  // the checked M = 2 form (5: 1024^3 3.38 vs 3.24 ms, profiles/r4q_checked_ab.jsonl)
+#define TSA_LAP_WPE2C 4
+#endif
 #ifndef TSA_LAP_LAUNDER
 #define TSA_LAP_LAUNDER 1
 #endif
@@ -484,7 +487,7 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 #define TSA_LAP_WPE1 6
 #endif
 __host__ __device__ constexpr int lap_waves_per_eu(int M, bool lit = false, bool chk = false) {
-  return lit ? (M == 1 ? 4 : 3) : M == 1 ? (chk ? 4 : TSA_LAP_WPE1) : M == 2 ? TSA_LAP_WPE2 : 2;
+  return lit ? (M == 1 ? 4 : 3) : M == 1 ? (chk ? 4 : TSA_LAP_WPE1) : M == 2 ? (chk ? TSA_LAP_WPE2C : TSA_LAP_WPE2) : 2;
 }
 // f(integral_constant<J>) for J = B .. E-1, unrolled at compile time
 template <int B, int E, class F>
@@ -1667,6 +1670,11 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
     delay = std::max(0.0, lap_steps - (lpr - 1.0) * (YOFF + LPD + 3)) * step * 1.5;
   }
   g.est_us = chain + (double)(std::max<int64_t>(g.waves, 1) - 1) * delay;
+  // refit on the round-4 runs (profiles/r4m_lapgeo.jsonl, r4j_lapab.jsonl):
+  // measured / estimated over several rounds is 0.69-0.90 for M = 1 (1024^3,
+  // 768^3, 8 x 512^3, 16 x 256^3) against 0.84-1.15 for M = 2; the factor puts
+  // 768^3 on M = 1 (1.90 vs 2.12 ms) and leaves the other three on M = 2
+  if (M == 1 && g.waves > 1) g.est_us *= 0.8;
   return g;
 }
 
