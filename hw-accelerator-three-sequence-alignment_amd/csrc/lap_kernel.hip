@@ -1565,9 +1565,13 @@ static int lap_blocks_per_cu_lit(size_t lds) {
 // M = 1 with two workgroups per CU (the latency-bound waves share SIMDs):
 // ~0.97 us per chained step (16 x 256^3 and 1024^3 in rounds,
 // profiles/r4c_lapab.jsonl), twice the one-per-CU step.
-static double lap_step_us(int M, int NW, int64_t wg_per_cu, bool lit = false) {
+static double lap_step_us(int M, int NW, int64_t wg_per_cu, bool lit = false, bool one_round = false) {
   const double base = M == 1 ? (NW == 4 ? 0.40 : 0.49) : M == 2 ? 0.62 : 1.45;
-  const double share = M == 1 ? 1.0 : 0.22;  // per extra workgroup on the CU
+  // per extra workgroup on the CU: two 9-wave M = 1 workgroups (4.5 waves per
+  // SIMD) ~double the step; two 5-wave ones in one resident round barely slow
+  // it (profiles/r4u_lap_nw.jsonl: 512^3 NW = 4 0.815 ms vs NW = 8 0.816,
+  // 384^3 0.568 vs 0.599, literal 512^3 1.046 vs 1.132)
+  const double share = M == 1 ? (NW == 4 && one_round ? 0.1 : 1.0) : 0.22;
   return (lit ? 1.6 : 1.0) * base * (1.0 + share * (double)(std::max<int64_t>(wg_per_cu, 1) - 1));
 }
 
@@ -1657,7 +1661,7 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   const int64_t wg_cu = std::max<int64_t>(1, std::min<int64_t>(per_cu, (wg_per_xcd + xcd_cus - 1) / xcd_cus));
   const double steps = (double)(g.G - 1) * (YOFF + LPD + 3) + (double)(g.GZ - 1) * (ZT + LPD + 2) +
                        (double)(max_la + YOFF + ZT);
-  const double step = lap_step_us(M, NW, wg_cu, lit);
+  const double step = lap_step_us(M, NW, wg_cu, lit, g.waves <= 1);
   const double chain = steps * step;
   // a slot's lap of round r + 1 starts when its lap of round r ends: one lap's
   // steps after its start, against (laps per round - 1) hand-offs of the chain
@@ -1670,11 +1674,14 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
     delay = std::max(0.0, lap_steps - (lpr - 1.0) * (YOFF + LPD + 3)) * step * 1.5;
   }
   g.est_us = chain + (double)(std::max<int64_t>(g.waves, 1) - 1) * delay;
-  // refit on the round-4 runs (profiles/r4m_lapgeo.jsonl, r4j_lapab.jsonl):
-  // measured / estimated over several rounds is 0.69-0.90 for M = 1 (1024^3,
-  // 768^3, 8 x 512^3, 16 x 256^3) against 0.84-1.15 for M = 2; the factor puts
-  // 768^3 on M = 1 (1.90 vs 2.12 ms) and leaves the other three on M = 2
-  if (M == 1 && g.waves > 1) g.est_us *= 0.8;
+  // refit on the round-4 runs (profiles/r4m_lapgeo.jsonl, r4j_lapab.jsonl,
+  // r4t_literal_geo.jsonl): measured / estimated over several rounds is
+  // 0.69-0.90 for M = 1 (1024^3 0.86, 768^3 0.90, 8 x 512^3 0.69, 16 x 256^3
+  // 0.74) and 0.72-0.76 for the literal M = 1 (1024^3, 768^3), against
+  // 0.84-1.15 for M = 2; the factors put 768^3 (1.90 vs 2.12 ms) and literal
+  // 1024^3 (4.10 vs 4.37) on M = 1 and leave 1024^3 (2.98 vs 3.08), 8 x 512^3
+  // and 16 x 256^3 on M = 2
+  if (M == 1 && g.waves > 1) g.est_us *= lit ? 0.7 : 0.8;
   return g;
 }
 
