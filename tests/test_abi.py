@@ -78,7 +78,7 @@ def test_workspace_size(tsa, monkeypatch):
     assert tsa.describe_plan(4, 64, 64, 64, p, kernel="plane").startswith("plane literal-lap")
     ll = tsa.workspace_size(1, 256, 256, 256, p, "plane")
     assert tsa.describe_plan(1, 512, 512, 512, p, kernel="plane").startswith("plane literal-lap")
-    assert 1.5 < tsa.workspace_size(1, 512, 512, 512, p, "plane") / ll < 6
+    assert 1.5 < tsa.workspace_size(1, 512, 512, 512, p, "plane") / ll < 12  # 512^3: two per CU
     monkeypatch.setenv("TSA_PENCIL_MODE", "plane")  # the plane sweep itself
     n1 = tsa.workspace_size(1, 64, 64, 64, p, "plane")
     n4 = tsa.workspace_size(4, 64, 64, 64, p, "plane")
@@ -184,10 +184,11 @@ def test_lap_rounds_and_ring_memory(tsa):
     # within one round: slim rings only (no boundary ring memory)
     p = tsa.TsaParams.default()
     assert "waves=1" in tsa.describe_plan(1, 512, 512, 512, p, sync=False)
-    assert tsa.workspace_size(1, 512, 512, 512, p, "pencil") <= 30e6
-    # O(N^2): 256^3 -> 512^3 grows ~4x at most
+    assert tsa.workspace_size(1, 512, 512, 512, p, "pencil") <= 100e6
+    # O(N^2): 256^3 -> 512^3 grows ~4x, x2 more where 512^3 runs two NW = 4
+    # workgroups per CU (their slim rings take 96 slots of slack, not 32)
     w256 = tsa.workspace_size(1, 256, 256, 256, p, "pencil")
-    assert tsa.workspace_size(1, 512, 512, 512, p, "pencil") / w256 < 4.5
+    assert tsa.workspace_size(1, 512, 512, 512, p, "pencil") / w256 < 9
 
 
 @pytest.mark.skipif(os.environ.get("TSA_EXPECT_GPU") == "1", reason="GPU box")
