@@ -172,6 +172,30 @@ def test_describe_plan(tsa):
     assert plan.startswith("pencil lap i16") and " chunk=" in plan and " checked" in plan, plan
 
 
+def test_lap_planner_measured_choices(tsa):
+    """The lap planner picks the geometries the round-4 sweeps measured fastest
+    (profiles/r4m_lapgeo.jsonl, r4t_literal_geo.jsonl,
+    r4u_lap_nw.jsonl, r4j_lapab.jsonl). Host-only (the CPU residency model)."""
+    p12 = tsa.TsaParams.default()
+    p16 = tsa.TsaParams.default(score_bits=16)
+
+    def geo(plan):
+        return re.search(r"M=(\d) NW=(\d)", plan).groups()
+
+    want = [
+        ((1, 768, p16, "pencil"), ("1", "8")),    # 1.90 ms vs M = 2 2.12
+        ((1, 1024, p16, "pencil"), ("2", "8")),   # 2.98 ms vs M = 1 3.08
+        ((8, 512, p12, "pencil"), ("2", "8")),    # 2.20 ms vs M = 1 2.69
+        ((16, 256, p12, "pencil"), ("2", "8")),   # 0.745 ms vs M = 1 0.847
+        ((1, 256, p12, "pencil"), ("1", "4")),
+        ((1, 1024, p12, "plane"), ("1", "8")),    # literal: 4.10 ms vs M = 2 4.37
+        ((1, 512, p12, "plane"), ("1", "4")),     # literal: 1.046 ms vs NW = 8 1.132
+    ]
+    for (n, L, p, k), mw in want:
+        plan = tsa.describe_plan(n, L, L, L, p, kernel=k, sync=False)
+        assert "lap" in plan and geo(plan) == mw, (n, L, k, plan)
+
+
 def test_lap_rounds_and_ring_memory(tsa):
     """A 1024^3 cube does not fit one round of resident lap workgroups, so it
     runs two rounds -- each workgroup looping over its slot's laps -- with
