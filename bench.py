@@ -162,17 +162,25 @@ def spawn_ranks(n: int, argv: list[str], script: str = __file__) -> int:
     return (abs(bad[0]) or 1) if bad else 0
 
 
-PROFILE_WARMUP, PROFILE_STEPS, PROFILE_SINGLE_REPS = 3, 10, 9
+# The profiled child runs the parent's --steps after at least PROFILE_WARMUP
+# warm-up launches (the first launches on a cold box run ~20 % long while the
+# clocks ramp: profiles/r4s per-dispatch trace 5.88 -> 4.77 ms over 9 launches);
+# roofline.frac comes from its per-dispatch trace of the timed launches only.
+PROFILE_WARMUP, PROFILE_SINGLE_REPS = 10, 9
+# profiled kernel time allowed above the live kernel time before the line flags it
+PROFILE_TOLERANCE = 1.03
 
 
 def run_profile_child(args) -> dict:
     """rocprofv3 --kernel-trace --stats over this same bench (the program
-    directly after --): a child process that runs PROFILE_WARMUP + PROFILE_STEPS
-    batch launches and PROFILE_SINGLE_REPS + 1 single configs[2] cubes on the
-    same box, before this process touches the GPU. Returns the stats rows of
-    the batch kernel and the single-cube lap kernel ({} with an "error" when
-    the profiler is absent or fails) and the csv path, so the line's
-    roofline.frac comes from the profiled average of this run's own box."""
+    directly after --): a child process that runs max(--warmup, PROFILE_WARMUP)
+    + --steps batch launches and the configs[2] single cube (1 + 2 x
+    PROFILE_SINGLE_REPS calls) on the same box, before this process touches the
+    GPU. Returns, per kernel, the per-dispatch durations of the timed window
+    only (timed_dispatches: the batch's warm-up launches dropped), the stats
+    summary of every launch under "stats" ({} with an "error" when the profiler
+    is absent or fails) and both csv paths, so the line's roofline.frac comes
+    from the profiled launches that correspond to the timed ones."""
     import csv
     import shutil
     import signal
@@ -181,9 +189,10 @@ def run_profile_child(args) -> dict:
         return {"error": "rocprofv3 not found"}
     out = os.path.abspath(args.profile_dir or os.path.join(ROOT, "gpurun_out", "bench_profile"))
     os.makedirs(out, exist_ok=True)
+    warm = max(args.warmup, PROFILE_WARMUP)
     cmd = [prof, "--kernel-trace", "--stats", "-d", out, "-o", "run", "--output-format", "csv", "--",
-           sys.executable, os.path.abspath(__file__), "--profile-child", "--steps", str(PROFILE_STEPS),
-           "--warmup", str(PROFILE_WARMUP), "--per-gpu", str(args.per_gpu), "--length", str(args.length),
+           sys.executable, os.path.abspath(__file__), "--profile-child", "--steps", str(args.steps),
+           "--warmup", str(warm), "--per-gpu", str(args.per_gpu), "--length", str(args.length),
            "--score-bits", str(args.score_bits), "--kernel", args.kernel, "--workload", args.workload]
     env = dict(os.environ, TMPDIR="/tmp")
     t0 = time.perf_counter()
@@ -201,20 +210,55 @@ def run_profile_child(args) -> dict:
         stats = os.path.join(out, "run_kernel_stats.csv")
         with open(stats) as f:
             rows = list(csv.DictReader(f))
+        trace = os.path.join(out, "run_kernel_trace.csv")
+        with open(trace) as f:
+            disp = list(csv.DictReader(f))
     except Exception as e:  # noqa: BLE001  (recorded: the line falls back to the live time)
         return {"error": str(e)[-300:]}
-    res = {"csv": os.path.relpath(stats, ROOT) if stats.startswith(ROOT) else stats,
+    rel = (lambda p: os.path.relpath(p, ROOT) if p.startswith(ROOT) else p)
+    res = {"csv": rel(stats), "trace_csv": rel(trace),
            "command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --profile-child "
-                      f"--steps {PROFILE_STEPS} --warmup {PROFILE_WARMUP}",
+                      f"--steps {args.steps} --warmup {warm}",
            "child_s": round(time.perf_counter() - t0, 1)}
-    for r in rows:
+    res.update(timed_dispatches(disp, warm, args.steps))
+    for r in rows:  # the stats summary (every launch, warm-ups included)
         name = r["Name"]
         for key in ("pencil_kernel", "lap_kernel", "plane_step_kernel", "literal_kernel"):
-            if f"tsa::{key}<" in name and key not in res:
-                res[key] = {"name": name.split("(")[0], "calls": int(r["Calls"]),
-                            "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
-                            "max_ns": float(r["MaxNs"])}
+            if f"tsa::{key}<" in name and key not in res.get("stats", {}):
+                res.setdefault("stats", {})[key] = {
+                    "name": name.split("(")[0], "calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                    "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"])}
     return res
+
+
+def timed_dispatches(rows, warmup: int, steps: int) -> dict:
+    """Per-dispatch durations (rocprofv3 --kernel-trace csv rows) of the
+    profiled child's launches, by kernel, in dispatch order: the batch kernel's
+    first `warmup` launches are dropped and the next `steps` kept -- exactly
+    the window the parent times -- and the single-cube lap kernel's first
+    launch (the untimed warm-up call) is dropped. Each kept kernel gets
+    {name, calls, avg_ns, median_ns, min_ns, max_ns, dispatch_ids, window}."""
+    import statistics
+    out = {}
+    by = {}
+    for r in sorted(rows, key=lambda r: int(r["Dispatch_Id"])):
+        name = r["Kernel_Name"]
+        for key in ("pencil_kernel", "lap_kernel", "plane_step_kernel", "literal_kernel"):
+            if f"tsa::{key}<" in name:
+                by.setdefault(key, []).append(
+                    (int(r["Dispatch_Id"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), name))
+    for i, (key, ds) in enumerate(by.items()):
+        # the first kernel family in dispatch order is the batch's
+        keep = ds[warmup:warmup + steps] if i == 0 else ds[1:]
+        window = (f"launches {warmup + 1}..{warmup + len(keep)} of {len(ds)} (warm-ups dropped)" if i == 0
+                  else f"launches 2..{len(ds)} (the untimed first call dropped)")
+        if not keep:
+            continue
+        ns = [d for _, d, _ in keep]
+        out[key] = {"name": keep[0][2].split("(")[0], "calls": len(ns), "avg_ns": float(statistics.mean(ns)),
+                    "median_ns": float(statistics.median(ns)), "min_ns": float(min(ns)),
+                    "max_ns": float(max(ns)), "dispatch_ids": [keep[0][0], keep[-1][0]], "window": window}
+    return out
 
 
 def profile_child_main(args) -> int:
@@ -303,6 +347,20 @@ class GpuBatch:
         return self.d_scores[: self.n]
 
 
+def fallback_counters(tsa) -> dict:
+    """The library's fallback counters (tsa_fallback_count: lap hand-offs that
+    timed out and were rescored without the lap schedule; tsa_check_fallback_count:
+    triples the checked kernel could not certify, rescored in the literal
+    arithmetic). Both count on the synchronous entry points; on the async path
+    the same events read as TSA_SCORE_INVALID / _UNCERTIFIED scores, which the
+    bench counts per timed call (invalid_reps)."""
+    return {"lap_timeouts": tsa.fallback_count(), "uncertified": tsa.check_fallback_count()}
+
+
+def counter_delta(c0: dict, c1: dict) -> dict:
+    return {k: c1[k] - c0[k] for k in c0}
+
+
 def run_rank(args, world: int, rank: int, local_rank: int, backend: str, make_batch,
              device=None, extras: bool = True, on_scores=None, prof=None):
     """One rank of the bench: shard, stage, warm up, time K steps between
@@ -343,6 +401,8 @@ def run_rank(args, world: int, rank: int, local_rank: int, backend: str, make_ba
     for _ in range(args.warmup):
         hot.step()
     hot.sync()
+    warm_scores = hot.scores().clone() if args.warmup > 0 else None
+    fb0 = fallback_counters(tsa)
     if world > 1:
         dist.barrier()
     hot.sync()
@@ -357,6 +417,13 @@ def run_rank(args, world: int, rank: int, local_rank: int, backend: str, make_ba
     hot.sync()
     elapsed = time.perf_counter() - t0
     kernel_ms_per_step = hot.elapsed_ms(ev0, ev1) / args.steps
+    # the timed launches ran the planned kernel: no fallback counted, and the
+    # last step's scores equal the warm-up's (a timed-out hand-off would read
+    # TSA_SCORE_INVALID on this async path)
+    batch_fb = counter_delta(fb0, fallback_counters(tsa))
+    sc = hot.scores()
+    batch_fb["invalid_scores"] = int((sc <= tsa.SCORE_UNCERTIFIED).sum().item()) if sc.numel() else 0
+    batch_fb["stable_vs_warmup"] = bool((sc == warm_scores).all().item()) if warm_scores is not None else None
     elapsed_max = shard.max_over_ranks(elapsed, dev)
 
     # what this rank saw: the collective's world (RCCL under "nccl") and the
@@ -381,6 +448,8 @@ def run_rank(args, world: int, rank: int, local_rank: int, backend: str, make_ba
         rec = report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gcups,
                      ms_per_step, kernel_ms_per_step, all_scores, extras, prof)
         rec["config"]["devices"] = devices
+        rec["config"]["split_devices"] = split_devices(args.gpus)
+        rec["fallbacks"] = fallback_summary(batch_fb, rec.get("single_cube") or {})
         if on_scores is not None:  # test hook: the gathered scores, global order
             on_scores(rec, all_scores)
     if world > 1:
@@ -429,6 +498,9 @@ def report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gc
         live = insts / kernel_s
         prof_s = kprof["avg_ns"] * 1e-9 if kprof else None
         ach = insts / prof_s if prof_s else live
+        # the profiled launches must describe the timed ones: flag a profiled
+        # mean more than PROFILE_TOLERANCE above the live kernel time
+        prof_ratio = round(prof_s / kernel_s, 4) if prof_s else None
         roofline = {"bound": "valu", "achieved": round(ach / 1e9, 2),
                     "peak": VALU_WAVE_INSTR_PER_S / 1e9, "unit": "G wave-instr/s",
                     "frac": round(ach / VALU_WAVE_INSTR_PER_S, 4),
@@ -442,10 +514,19 @@ def report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gc
                                          / VALU_WAVE_INSTR_PER_S, 4),
                     "algorithmic_note": f"value/n_gpus x {CORE_LANE_OPS_PER_CELL} lane-ops per cell "
                                         "(cell_messages_vs pair core) / (64 x peak)",
+                    "profiled_ms": round(prof_s * 1e3, 4) if prof_s else None,
+                    "profiled_median_ms": round(kprof["median_ns"] * 1e-6, 4) if kprof else None,
+                    "profiled_window": kprof.get("window") if kprof else None,
+                    "profiled_over_live": prof_ratio,
+                    "profile_consistent": (prof_ratio <= PROFILE_TOLERANCE) if prof_ratio else None,
                     "source": (f"SQ_INSTS_VALU per launch (profiles/pmc_{kernel_name}_{args.workload}.json)"
-                               " / " + ("rocprofv3 average of the profiled child (profile)" if prof_s
-                                        else "live kernel time (HIP events; no profile: "
+                               " / " + ("mean per-dispatch duration of the profiled child's timed window "
+                                        "(rocprofv3 --kernel-trace, warm-ups dropped; profile.trace_csv)"
+                                        if prof_s else "live kernel time (HIP events; no profile: "
                                         + str(prof.get("error", "skipped")) + ")"))}
+        if prof_ratio and prof_ratio > PROFILE_TOLERANCE:
+            log(f"roofline: profiled kernel {prof_s * 1e3:.4f} ms is {prof_ratio:.3f} x the live "
+                f"{kernel_ms_per_step:.4f} ms (> {PROFILE_TOLERANCE}): flagged (profile_consistent false)")
     else:  # no current profile: the contract's HBM form on algorithmic bytes
         roofline = dict(hbm_model, traffic=traffic)
     roofline.update({"kernel": kernel_name, "kernel_ms_per_step": round(kernel_ms_per_step, 4),
@@ -493,6 +574,18 @@ def report(args, tsa, synth, hot, dev, world, n_total, per_gpu, n, L, params, gc
         "parity": parity,
         "build": tsa.build_info(),
     }
+
+
+def fallback_summary(batch_fb: dict, single: dict) -> dict:
+    """Every fallback the timed work could have taken, in one place: the batch
+    step's counter deltas and score checks, each single cube's, and all_zero
+    (true when no counter moved and no timed call read an invalid score)."""
+    singles = {k: v["fallbacks"] for k, v in single.items() if isinstance(v, dict) and "fallbacks" in v}
+    vals = [batch_fb] + list(singles.values())
+    zero = all(d.get("lap_timeouts", 0) == 0 and d.get("uncertified", 0) == 0
+               and d.get("invalid_scores", d.get("invalid_reps", 0)) == 0 for d in vals)
+    zero = zero and batch_fb.get("stable_vs_warmup") is not False
+    return {"batch": batch_fb, "single_cube": singles, "all_zero": zero}
 
 
 def lap_roofline(args, L, single, prof) -> dict | None:
@@ -583,6 +676,8 @@ def time_singles(args, tsa, synth, hot, dev, L, params, reps=None):
                     SPIN_OK[0] = False
             hot.step()
 
+        rep_scores = []
+
         def timed(preload):
             # preload: a spin kernel queued first keeps the GPU busy while the
             # host submits e0, the cube's launch(es) and e1, so e0 -> e1 is the
@@ -600,7 +695,9 @@ def time_singles(args, tsa, synth, hot, dev, L, params, reps=None):
                 e1.record(stream)
                 torch.cuda.synchronize()
                 times.append(e0.elapsed_time(e1))
+                rep_scores.append(int(s_score.item()))  # every timed call's own score
             return float(np.median(times))
+        fb0 = fallback_counters(tsa)
         sms = timed(preload=hot.n > 0)
         r = {"ms": round(sms, 4), "gcups": round(la * lb * lc / (sms * 1e-3) / 1e9, 3),
              "score": int(s_score.item()), "score_bits": prm.score_bits,
@@ -609,6 +706,16 @@ def time_singles(args, tsa, synth, hot, dev, L, params, reps=None):
                        "spin kernel so host submission is hidden" if hot.n > 0 else "events, host submit included"}
         if hot.n > 0:
             r["ms_incl_submit"] = round(timed(preload=False), 4)
+        # the timed calls ran the planned kernel: counters unmoved, no call
+        # read TSA_SCORE_INVALID (a timed-out hand-off on this async path), and
+        # every call scored the same
+        fb = counter_delta(fb0, fallback_counters(tsa))
+        bad = sum(1 for v in rep_scores if v == tsa.SCORE_INVALID or
+                  (v == tsa.SCORE_UNCERTIFIED and kernel != "checked"))
+        fb.update({"timed_calls": len(rep_scores), "invalid_reps": bad,
+                   "uncertified_reps": sum(1 for v in rep_scores if v == tsa.SCORE_UNCERTIFIED),
+                   "scores_agree": len(set(rep_scores)) <= 1})
+        r["fallbacks"] = fb
         if Ls in ASIC_MS and prm.score_bits == 12 and trip is None:
             r["asic_ms"] = ASIC_MS[Ls]
             r["vs_asic"] = round(ASIC_MS[Ls] / sms, 3)
@@ -634,11 +741,17 @@ def time_singles(args, tsa, synth, hot, dev, L, params, reps=None):
     return out
 
 
+def split_devices(world_devices: int) -> str:
+    """Devices the split-over-devices leg lays one cube over: 2 parts sharing
+    device 0 at N = 1, devices 0..N-1 on an N-GPU run."""
+    return ",".join(str(d) for d in range(world_devices)) if world_devices > 1 else "0,0"
+
+
 def time_split(world_devices: int) -> dict:
     """One cube split over devices by laps, in a child
     process with its own time limit: 2 parts sharing device 0 at N = 1,
     devices 0..N-1 on an N-GPU run (rank 0, while the other ranks wait)."""
-    devs = ",".join(str(d) for d in range(world_devices)) if world_devices > 1 else "0,0"
+    devs = split_devices(world_devices)
     cmd = [sys.executable, os.path.join(ROOT, "tools", "split_cube.py"), "--devices", devs,
            "--lengths", SPLIT_LENGTHS]
     try:

@@ -45,11 +45,14 @@
 //    hold 2-4x the natural lag);
 //  * block b -> XCD b % 8 (observed dispatch, speed only): every lap of a z-tile
 //    lands on one XCD, so the y chain's hand-offs stay in one L2's reach.
-// A consumer only waits on workgroups of lower block index (lap-major order),
-// and a producer waits (back-pressure) only on a consumer of its own dispatch
-// round -- across a round boundary its ring is full length -- so a grid beyond
-// the resident slots is safe with per-XCD in-order dispatch (measured, not
-// promised by HIP; every wait is bounded and reports).
+// A consumer only waits on laps of lower index (lap-major order), and a
+// producer waits (back-pressure) only on a consumer of its own round -- across
+// a round boundary its ring is full length. A grid beyond the resident slots is
+// launched as one resident round (8 x SX workgroups) whose workgroups loop over
+// their slots' later-round laps in lap order (up to LAP_MAX_WAVES rounds, any
+// workgroups per CU), so no wait depends on the dispatcher's order; forward
+// progress needs every launched workgroup co-resident (every wait is bounded
+// and reports TSA_SCORE_INVALID).
 
 #include <unistd.h>
 
@@ -486,6 +489,13 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 #ifndef TSA_LAP_WPE1
 #define TSA_LAP_WPE1 6
 #endif
+// wave 0 reads only the payload words of its tagged y record (ds_read2_b32):
+// a 16-byte read hands the compiler the two dead tag registers, which it
+// reuses before the read has landed -- a write-after-write wait that puts
+// the record read's latency in front of the pre-cell
+#ifndef TSA_LAP_Y2
+#define TSA_LAP_Y2 0
+#endif
 __host__ __device__ constexpr int lap_waves_per_eu(int M, bool lit = false, bool chk = false) {
   return lit ? (M == 1 ? 4 : 3) : M == 1 ? (chk ? 4 : TSA_LAP_WPE1) : M == 2 ? (chk ? TSA_LAP_WPE2C : TSA_LAP_WPE2) : 2;
 }
@@ -650,8 +660,9 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
   const int32_t T = final_wg ? (la - 1 + LX) + tau(r_f) + k_f + 1 : la + LX + tau(rows - 1) + zt_q - 1;
   const int32_t T_above = la + LX + tau(RW - 1) + zt_q - 1;  // records the lap above writes (same tile)
   const int32_t T_left = la + LX + tau(rows - 1) + ZT - 1;   // z records the tile to the left writes
-  // Rings. A grid beyond the resident slots runs in dispatch rounds (per XCD,
-  // in block order: rd.SX slots each). A producer whose consumer is in a later
+  // Rings. A grid beyond the resident slots runs in rounds of rd.SX slots per
+  // XCD, each resident workgroup looping over its slots in lap order (the
+  // slot loop at the end of lap_kernel). A producer whose consumer is in a later
   // round gets a full-length ring from the boundary region (it never waits
   // for a consumer that may not have started); all others a slim ring of
   // YR / ZR slots, their consumers co-resident (lap_geom).
@@ -1116,8 +1127,20 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
       const uint8_t *src = ROLE == 0 ? ysrc + (t & (K0 - 1)) * ystride
                                      : xr + ((w - 1) * K + ((t - 1) & (K - 1))) * SLOT + lane * REC_BYTES;
       uint4 rv[M];
+      auto read_rec = [&]() {
 #pragma unroll
-      for (int i = 0; i < M; ++i) rv[i] = lds_read16(src + i * PAIR);
+        for (int i = 0; i < M; ++i) {
+          if constexpr (ROLE == 0 && TSA_LAP_Y2) {  // {payload, tag, payload, tag}: the payloads only
+            const __attribute__((address_space(3))) uint32_t *p =
+                (const __attribute__((address_space(3))) uint32_t *)(const __attribute__((address_space(3))) void *)(
+                    src + i * PAIR);
+            rv[i] = make_uint4(p[0], 0u, p[2], 0u);
+          } else {
+            rv[i] = lds_read16(src + i * PAIR);
+          }
+        }
+      };
+      read_rec();
       // the successor's progress, read now and consulted before the record store
       int32_t succ_v = 0;
       if constexpr (ROLE != 2)
@@ -1207,8 +1230,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
         if (seen_in < need) {
           wait_word(pword, seen_in, need);
           asm volatile("" ::: "memory");
-#pragma unroll
-          for (int i = 0; i < M; ++i) rv[i] = lds_read16(src + i * PAIR);
+          read_rec();
         }
       }
       // ---- the row above of both halves
@@ -1505,11 +1527,15 @@ int lap_simd_blocks_per_cu(int M, int NW, bool f16, bool sop, bool lit) {
   slot.store(r + 1, std::memory_order_relaxed);
   return r;
 }
-// Workgroups of one instantiation a CU holds, from the HIP occupancy API on the
-// real kernel (VGPRs, LDS) capped by the SGPR bound (the API reads one block
-// high at 81-112 SGPRs); without a device, the LDS / wave-slot model.
-// Memoized per (device, LDS bytes): a single-cube call plans a dozen
-// geometries, and each occupancy query is host latency on that call.
+// Workgroups of one shape a CU holds, from the HIP occupancy API on the real
+// kernels (VGPRs, LDS) capped by the SGPR bound (the API reads one block high
+// at 81-112 SGPRs); without a device, the LDS / wave-slot model. The API is
+// asked about every instantiation the plan can launch -- the plain kernel, the
+// checked (CHK) one of the int16 form and the V-space (VS) one of the f16
+// form -- and the least count stands, so the looped grid's residency holds
+// whichever of them runs. Memoized per (device, LDS bytes): a single-cube call
+// plans a dozen geometries, and each occupancy query is host latency on that
+// call.
 template <int M, int NW, bool F16, bool SOP, bool LIT = false>
 static int lap_blocks_per_cu_t(size_t lds) {
   struct Entry {
@@ -1528,8 +1554,15 @@ static int lap_blocks_per_cu_t(size_t lds) {
       for (const Entry &e : memo)
         if (e.dev == dev && e.lds == lds) return e.nb;
     }
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, lap_kernel<M, NW, F16, SOP, false, false, LIT>,
-                                                     64 * (NW + 1), lds) == hipSuccess) {
+    auto query = [&](auto kfn) -> int {
+      int k = 0;
+      return hipOccupancyMaxActiveBlocksPerMultiprocessor(&k, kfn, 64 * (NW + 1), lds) == hipSuccess ? k : -1;
+    };
+    nb = query(lap_kernel<M, NW, F16, SOP, false, false, LIT>);
+    if (nb >= 0) {
+      if constexpr (!F16 && !LIT) nb = std::min(nb, std::max(0, query(lap_kernel<M, NW, false, SOP, true>)));
+      if constexpr (F16 && !LIT)
+        nb = std::min(nb, std::max(0, query(lap_kernel<M, NW, true, SOP, false, false, false, true>)));
       nb = std::min(nb, sg);
       std::lock_guard<std::mutex> g(mu);
       if (memo.size() < 4096) memo.push_back(Entry{dev, lds, nb});
@@ -1556,7 +1589,8 @@ static int lap_blocks_per_cu_lit(size_t lds) {
              : ((NW_) == 4 ? TSA_LIT_SOP(FN, 2, 4, SOP_, __VA_ARGS__) : TSA_LIT_SOP(FN, 2, 8, SOP_, __VA_ARGS__)))
 
 // Step time (us) along the chain, fitted on MI355X to single cubes
-// (scripts/gpu_lapvar.sh, tools/lap_trace.py; DESIGN.md 4.4: 64^3..1024^3
+// (geometry sweeps profiles/r4m_lapgeo.jsonl, r4u_lap_nw.jsonl via
+// scripts/gpu_lapgeo.sh; tools/lap_trace.py; DESIGN.md 4.4: 64^3..1024^3
 // within ~10 %) and to batches of 4..128 cubes (profiles/r3o_chunk.jsonl:
 // M = 4, 16 x 256^3 .. 4 x 1024^3), growing with the workgroups per CU -- the
 // chain steps include the hand-off stalls.
@@ -1751,8 +1785,6 @@ static int launch_lap_fn(LapKernelFn kfn, int NW, const uint8_t *d_seqs, const i
   if (g.prog_bytes > ga.prog_bytes || g.yf_bytes > ga.yf_bytes || g.zf_bytes > ga.zf_bytes ||
       g.yb_bytes > ga.yb_bytes || g.zb_bytes > ga.zb_bytes)
     return TSA_EINTERNAL;  // a chunk's regions must fit the batch's
-  if (set_dynamic_lds((const void *)kfn, g.lds) != hipSuccess)
-    return TSA_EDEVICE;
   int32_t *prog = (int32_t *)d_ws;
   uint32_t *err = lap_err_word(ga, n, d_ws);
   int32_t *mon = chk ? (int32_t *)err + 64 : aux;  // [max(best)] n, [min(best)] n
@@ -1772,9 +1804,11 @@ static int launch_lap_fn(LapKernelFn kfn, int NW, const uint8_t *d_seqs, const i
   const uint32_t epoch = lap_next_epoch();
   const LapKArgs ka{d_seqs, d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, rd, prog, err,
                     d_scores, mon, pa, epoch, lap_spin_limit(), 0, g.G, yf, prog, trace, lit};
-  hipLaunchKernelGGL(kfn, dim3((uint32_t)g.grid), dim3(64 * (NW + 1)), g.lds, stream, LAP_KARGS(ka));
+  if (launch_with_lds((const void *)kfn, g.lds, [&] {
+        hipLaunchKernelGGL(kfn, dim3((uint32_t)g.grid), dim3(64 * (NW + 1)), g.lds, stream, LAP_KARGS(ka));
+      }) != hipSuccess)
+    return TSA_EDEVICE;
   if (chk) {
-    if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
     hipLaunchKernelGGL(lap_certify, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, mon, n,
                        *chk, d_scores);
   }
@@ -1887,8 +1921,6 @@ static int launch_split_fn(LapKernelFn kfn, int NW, const LapGeom &g, const Penc
   for (int p = 0; p < np; ++p) {
     const LapPart &q = parts[p];
     if (hipSetDevice(q.device) != hipSuccess) return TSA_EDEVICE;
-    if (set_dynamic_lds((const void *)kfn, g.lds) != hipSuccess)
-      return TSA_EDEVICE;
     int32_t *prog = (int32_t *)q.d_ws;
     uint8_t *yf = (uint8_t *)q.d_ws + g.prog_bytes;
     uint8_t *zf = yf + g.yf_bytes;
@@ -1898,8 +1930,10 @@ static int launch_split_fn(LapKernelFn kfn, int NW, const LapGeom &g, const Penc
     const LapKArgs ka{q.d_seqs, q.d_offsets, g.G, g.GZ, g.NC, g.CH, g.YR, g.ZR, yf, zf, lap_rounds(g, q.d_ws),
                       prog, d_err, d_score, (int32_t *)nullptr, pa, epoch, spin, q.L0, q.L1, yf_out, prog_in,
                       (unsigned long long *)nullptr, lit};
-    hipLaunchKernelGGL(kfn, dim3((uint32_t)blocks), dim3(64 * (NW + 1)), g.lds, q.stream, LAP_KARGS(ka));
-    if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
+    if (launch_with_lds((const void *)kfn, g.lds, [&] {
+          hipLaunchKernelGGL(kfn, dim3((uint32_t)blocks), dim3(64 * (NW + 1)), g.lds, q.stream, LAP_KARGS(ka));
+        }) != hipSuccess)
+      return TSA_EDEVICE;
   }
   return TSA_OK;
 }

@@ -536,12 +536,13 @@ static int launch_lit(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n
                       hipStream_t stream) {
   const int32_t lds_a = 4 * (g.P + 128 * M), lds_b = 4 * ((max_lb + 4) & ~3);
   auto kfn = literal_kernel<M, SOP>;
-  if (set_dynamic_lds((const void *)kfn, g.lds) != hipSuccess)
-    return TSA_EDEVICE;
   const int grid = n < 65535 ? n : 65535;
-  hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * LIT_NW), g.lds, stream, d_seqs, d_offsets, n, g.P, g.R, lds_a,
-                     lds_b, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, d_final7, ca);
-  return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
+  return launch_with_lds((const void *)kfn, g.lds, [&] {
+           hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * LIT_NW), g.lds, stream, d_seqs, d_offsets, n, g.P, g.R,
+                              lds_a, lds_b, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, d_final7, ca);
+         }) == hipSuccess
+             ? TSA_OK
+             : TSA_EDEVICE;
 }
 
 int literal_launch_batch(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n, int32_t max_la,

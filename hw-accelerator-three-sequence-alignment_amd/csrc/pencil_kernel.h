@@ -20,8 +20,10 @@ bool pencil_shape_supported(int32_t max_la, int32_t max_lb, int32_t max_lc);
 //   LAP_RESIDENT -- the lap kernel (async path);
 //   LAP_STREAM   -- the same plans on the synchronous paths, which check
 //                   *d_err after the launch and rescore with LAP_OFF.
-// Both run grids of up to LAP_MAX_WAVES dispatch rounds with boundary rings
-// (lap_geom); a lap launch that times out reports TSA_SCORE_INVALID.
+// Both run grids of up to LAP_MAX_WAVES rounds with boundary rings (lap_geom),
+// launched as one resident round whose workgroups loop over their later-round
+// laps in lap order (any workgroups per CU; every launched workgroup must be
+// co-resident); a lap launch that times out reports TSA_SCORE_INVALID.
 enum LapPolicy { LAP_OFF = 0, LAP_RESIDENT = 1, LAP_STREAM = 2 };
 // Certification limits of the checked kernel (DESIGN.md 1.2 with the observed
 // range of best in place of the a-priori one): a triple's scores stand when

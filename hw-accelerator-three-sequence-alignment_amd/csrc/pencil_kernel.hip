@@ -56,6 +56,25 @@ __host__ __device__ constexpr int helix_pd(int M) { return M >= 8 ? 2 : M >= 4 ?
 // skew and record slots per wave; M >= 4 keeps skew 1 (twice the slots would not fit LDS)
 __host__ __device__ constexpr int helix_skew(int M) { return M <= 2 ? TSA_SKEW : 1; }
 constexpr int RING_EXTRA = 8;
+// Ablation knobs (timing diagnostics only: the scores are WRONG when set):
+// TSA_ABL_ZOWN / TSA_ABL_ZREC replace the DPP + v_perm z-shift of the own
+// (Iz, Ixz) / the row-above (Iyz, M) messages by register moves, TSA_ABL_INJ
+// drops the x = 1 injection -- how much of the step each costs.
+#ifndef TSA_ABL_ZOWN
+#define TSA_ABL_ZOWN 0
+#endif
+#ifndef TSA_ABL_ZREC
+#define TSA_ABL_ZREC 0
+#endif
+#ifndef TSA_ABL_INJ
+#define TSA_ABL_INJ 0
+#endif
+template <int M>
+__device__ __forceinline__ void zmove_abl(uint32_t (&v)[M], const uint32_t (&src)[M]) {
+#pragma unroll
+  for (int i = M - 1; i >= 1; --i) v[i] = src[i - 1];
+  v[0] = src[M - 1];
+}
 // A-table entries past P + 128M repeating its start (the table is periodic in
 // P): the V-space loop reads a four-step group's A codes at constant offsets
 // from one address computed at the group's start, across a lap wrap too
@@ -90,11 +109,12 @@ static PencilGeom pencil_geom(int32_t max_la, int32_t max_lc) {
   g.ring_bytes_per_triple = (int64_t)g.R * g.M * 64 * REC_BYTES;
   return g;
 }
-static size_t helix_lds(int M, int NW, int32_t P, int32_t max_lb) {
-  // M = 2 (TSA_A_B64): the A table's copy shifted by one entry after fin
+// vs: the V-space instantiation, whose M = 2 form (TSA_A_B64) also keeps the
+// A table's copy shifted by one entry after fin; the other forms do not
+static size_t helix_lds(int M, int NW, int32_t P, int32_t max_lb, bool vs) {
   const size_t a_tab = 4 * ((size_t)P + 128 * M + A_PAD);
   return (size_t)(NW - 1) * 2 * helix_skew(M) * M * 1024 + (size_t)helix_pd(M) * M * 1024 + a_tab +
-         4 * (((size_t)max_lb + 3) & ~(size_t)3) + (size_t)M * 512 + (M == 2 && TSA_A_B64 ? a_tab : 0);
+         4 * (((size_t)max_lb + 3) & ~(size_t)3) + (size_t)M * 512 + (vs && M == 2 && TSA_A_B64 ? a_tab : 0);
 }
 
 // The factored messages widen each target's highest-penalty group to all seven
@@ -106,7 +126,9 @@ static bool pencil_shape_ok(int32_t max_la, int32_t max_lb, int32_t max_lc) {
         max_lc <= MAX_LC))
     return false;
   const PencilGeom g = pencil_geom(max_la, max_lc);
-  return helix_lds(g.M, helix_nw(g.M), g.P, max_lb) <= LDS_MAX;  // the helix is always runnable
+  // the helix is always runnable: the non-V-space form (use_vs admits the
+  // V-space one only where its own footprint fits too)
+  return helix_lds(g.M, helix_nw(g.M), g.P, max_lb, false) <= LDS_MAX;
 }
 
 static bool use_f16(const KParams &kp, const Range &r);
@@ -126,7 +148,7 @@ static double helix_est(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_l
   const PencilGeom g = pencil_geom(max_la, max_lc);
   const int nw = helix_nw(g.M);
   const int64_t per_cu = std::max<int64_t>(
-      1, std::min<int64_t>(LDS_MAX / helix_lds(g.M, nw, g.P, max_lb), waves_per_cu(g.M) / nw));
+      1, std::min<int64_t>(LDS_MAX / helix_lds(g.M, nw, g.P, max_lb, g.M == 2), waves_per_cu(g.M) / nw));
   const double T = (double)((max_lb - 1) / nw) * g.P + max_la + nw + max_lc;
   const int64_t units = g.two ? (n + 1) / 2 : n;
   return (double)((units + 256 * per_cu - 1) / (256 * per_cu)) * T *
@@ -479,7 +501,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       // ---- x == 1 at position k* = (t - w) mod P: its x-1 inputs are the x = 0
       // face (EN_i==1&&EN==0 gating, src/PE_1cyc.v:164-178,196-202,212-218), and
       // it starts row lap0*NW+w+1, whose B symbol it takes here.
-      if (TSA_HM_TRACK || xpos0 < KS) {  // (tracked: hmCur is 0 past KS)
+      if (!TSA_ABL_INJ && (TSA_HM_TRACK || xpos0 < KS)) {  // (tracked: hmCur is 0 past KS)
         int32_t ls, is, hs;
         pos_split<M>(xpos0, ls, is, hs);
 #if TSA_HM_TRACK
@@ -640,10 +662,20 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         advance();
         // z = 0 faces of position 0: (x, y, 0) and (x, y-1, 0) at step t+1,
         // (x-1, y, 0) and (x-1, y-1, 0) at step t+2
-        zshift<M>(shIxz[PH], oIxz, sel, Hr[(PQ + 2) & 3]);
-        zshift<M>(shIz, oIz, sel, Hr[(PQ + 1) & 3]);
-        zshift<M>(svIyz, rz, sel, Hr[(PQ + 1) & 3]);
-        zshift<M>(svM[PH], rw, sel, Hr[(PQ + 1) & 3]);
+        if constexpr (TSA_ABL_ZOWN) {
+          zmove_abl<M>(shIxz[PH], oIxz);
+          zmove_abl<M>(shIz, oIz);
+        } else {
+          zshift<M>(shIxz[PH], oIxz, sel, Hr[(PQ + 2) & 3]);
+          zshift<M>(shIz, oIz, sel, Hr[(PQ + 1) & 3]);
+        }
+        if constexpr (TSA_ABL_ZREC) {
+          zmove_abl<M>(svIyz, rz);
+          zmove_abl<M>(svM[PH], rw);
+        } else {
+          zshift<M>(svIyz, rz, sel, Hr[(PQ + 1) & 3]);
+          zshift<M>(svM[PH], rw, sel, Hr[(PQ + 1) & 3]);
+        }
       } else {
         zshift<M>(shIxz[PH], oIxz, sel, pa.f_pair);  // z = 0 face for position 0
         zshift<M>(shIz, oIz, sel, pa.f_single);
@@ -849,6 +881,8 @@ static bool use_vs(const KParams &kp, const Range &r, int32_t max_la, int32_t ma
     if (!strcmp(e, "i16") || !strcmp(e, "f16")) return false;
   const int32_t GE = kp.pen[SIXY][SIX], GO = kp.pen[SIXY][SM];
   if (!use_f16(kp, r) || pencil_pairs(max_lc) > 2 || GE < 1 || GE != -kp.mismatch || GO < GE) return false;
+  const PencilGeom g = pencil_geom(max_la, max_lc);
+  if (helix_lds(g.M, helix_nw(g.M), g.P, max_lb, true) > LDS_MAX) return false;  // the shifted A copy
   const int64_t slack = pencil_slack(kp.match, kp.mismatch, GO, GE);
   const int64_t hi = r.hi + (int64_t)GE * ((int64_t)max_la + max_lb + max_lc) + slack;
   return r.lo - slack >= -2048 && hi <= 2048 && (int64_t)GO + GE + kp.mismatch <= 2048;
@@ -881,20 +915,20 @@ static int launch_m(const uint8_t *d_seqs, const int64_t *d_offsets, int32_t n,
   constexpr bool VSOK = F16 && M <= 2;  // V-space instantiations
   const bool vs = VSOK && pa.lam != 0;
   const int32_t lds_a = 4 * (g.P + 128 * M + A_PAD), lds_b = 4 * ((max_lb + 3) & ~3);
-  const size_t lds = helix_lds(M, NW, g.P, max_lb);
+  const size_t lds = helix_lds(M, NW, g.P, max_lb, vs);
   // TWO (two triples per workgroup) exactly when pencil_geom sized P for it
   const bool two = M == 1 && g.two;
   auto kfn = vs ? (two ? pencil_kernel<M, NW, F16, SOP, M == 1, VSOK> : pencil_kernel<M, NW, F16, SOP, false, VSOK>)
                 : (two ? pencil_kernel<M, NW, F16, SOP, M == 1, false> : pencil_kernel<M, NW, F16, SOP, false, false>);
   if (lds > LDS_MAX) return TSA_EINVAL;
-  if (set_dynamic_lds((const void *)kfn, lds) != hipSuccess)
-    return TSA_EDEVICE;
   const int32_t units = two ? (n + 1) / 2 : n;
   const int grid = units < 65535 ? units : 65535;
-  hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * NW), lds, stream, d_seqs, d_offsets, n, g.P,
-                     g.R, lds_a, lds_b, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores,
-                     pa);
-  return hipGetLastError() == hipSuccess ? TSA_OK : TSA_EDEVICE;
+  return launch_with_lds((const void *)kfn, lds, [&] {
+           hipLaunchKernelGGL(kfn, dim3(grid), dim3(64 * NW), lds, stream, d_seqs, d_offsets, n, g.P, g.R, lds_a,
+                              lds_b, g.ring_bytes_per_triple, (uint8_t *)d_ws, d_scores, pa);
+         }) == hipSuccess
+             ? TSA_OK
+             : TSA_EDEVICE;
 }
 
 void pencil_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, const KParams &kp,
@@ -907,8 +941,8 @@ void pencil_describe(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, 
     if (f16 && lap_vs_ok(kp, bound, max_la, max_lb, max_lc)) arith = "f16v";  // the lap's V-space cell
     char chunk[32] = "";
     if (lg.chunk > 0) snprintf(chunk, sizeof chunk, " chunk=%d", lg.chunk);
-    snprintf(buf, len, "pencil lap %s %s M=%d NW=%d laps=%d tiles=%d waves=%lld%s%s est=%.0fus", arith, s3, lg.M,
-             lg.NW, lg.G, lg.GZ, (long long)lg.waves, chunk, checked ? " checked" : "", lg.est_us);
+    snprintf(buf, len, "pencil lap %s %s M=%d NW=%d laps=%d tiles=%d waves=%lld wpc=%d%s%s est=%.0fus", arith, s3,
+             lg.M, lg.NW, lg.G, lg.GZ, (long long)lg.waves, lg.per_cu, chunk, checked ? " checked" : "", lg.est_us);
     return;
   }
   const PencilGeom g = pencil_geom(max_la, max_lc);

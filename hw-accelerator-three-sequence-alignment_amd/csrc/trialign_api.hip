@@ -187,14 +187,26 @@ int tsa_validate(const uint8_t *a, int32_t la, const uint8_t *b, int32_t lb, con
 
 namespace tsa {
 
+namespace {
+struct LdsEntry {
+  const void *fn;
+  int dev;
+  size_t lds;
+};
+std::mutex lds_mu;
+std::vector<LdsEntry> lds_done;
+}  // namespace
+
+void forget_dynamic_lds(const void *fn) {
+  std::lock_guard<std::mutex> g(lds_mu);
+  lds_done.erase(std::remove_if(lds_done.begin(), lds_done.end(), [&](const LdsEntry &e) { return e.fn == fn; }),
+                 lds_done.end());
+}
+
 hipError_t set_dynamic_lds(const void *fn, size_t lds) {
-  struct Entry {
-    const void *fn;
-    int dev;
-    size_t lds;
-  };
-  static std::mutex mu;
-  static std::vector<Entry> done;
+  using Entry = LdsEntry;
+  std::mutex &mu = lds_mu;
+  std::vector<Entry> &done = lds_done;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = -1;
   {

@@ -53,6 +53,24 @@ void bound_drops(const tsa_params *p, int64_t *drop, int64_t *cdrop);
 // least `lds` bytes (a per-launch attribute call is host latency on every
 // single-cube call). hipSuccess or the HIP error.
 hipError_t set_dynamic_lds(const void *fn, size_t lds);
+// Drop `fn`'s cached entries (every device): the next set_dynamic_lds sets the
+// attribute again.
+void forget_dynamic_lds(const void *fn);
+// set_dynamic_lds + launch() (a hipLaunchKernelGGL of fn with `lds` dynamic
+// bytes). A cached attribute can be stale -- hipDeviceReset drops it while the
+// cache still skips the call -- so a failed launch forgets the entry, sets the
+// attribute afresh and launches once more. hipSuccess or the HIP error.
+template <class F>
+hipError_t launch_with_lds(const void *fn, size_t lds, F &&launch) {
+  hipError_t rc = set_dynamic_lds(fn, lds);
+  if (rc != hipSuccess) return rc;
+  launch();
+  if ((rc = hipGetLastError()) == hipSuccess) return rc;
+  forget_dynamic_lds(fn);
+  if ((rc = set_dynamic_lds(fn, lds)) != hipSuccess) return rc;
+  launch();
+  return hipGetLastError();
+}
 
 // Row stride (cells) of a (y,z) plane with lc+1 columns.
 inline int64_t plane_ldz(int64_t lc) { return lc + 1; }

@@ -147,12 +147,15 @@ int tsa_score_batch_devices(const uint8_t *seqs, const int64_t *offsets, int32_t
  * symbols is the caller's job on this path (tsa_validate on the host copy).
  * For a few large cubes this path may run the single-cube (lap) schedule --
  * the factored lap kernel, or for TSA_KERNEL_PLANE the literal lap kernel --
- * whose workgroups hand data to each other. Its grid may span several
- * dispatch rounds (up to three, one workgroup per CU); that relies on the
- * in-order per-XCD workgroup dispatch measured on MI355X, which HIP does not
- * promise. Every hand-off wait is bounded: if one times out, the affected
- * triples read TSA_SCORE_INVALID once the stream has synchronised -- check
- * for it on every kernel choice, TSA_KERNEL_PLANE included. */
+ * whose workgroups hand data to each other. The launched grid is one
+ * resident round (8 x SX workgroups, at any workgroups per CU); a cube or
+ * batch with more laps than resident slots runs up to LAP_MAX_WAVES (4)
+ * rounds as each workgroup's loop over its later-round laps, in lap order.
+ * Forward progress needs every launched workgroup co-resident, so a
+ * concurrent kernel holding CUs of the device can delay some of them; every
+ * hand-off wait is bounded, and if one times out the affected triples read
+ * TSA_SCORE_INVALID once the stream has synchronised -- check for it on every
+ * kernel choice, TSA_KERNEL_PLANE included. */
 int tsa_batch_workspace_size(int32_t n, int32_t max_la, int32_t max_lb,
                              int32_t max_lc, const tsa_params *p,
                              int32_t kernel, size_t *bytes);

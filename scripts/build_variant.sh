@@ -13,11 +13,19 @@ SRC=${SRC:-$PKG}  # source tree (e.g. a git archive of an older commit)
 OUT=variants/$NAME
 rm -rf "$OUT"; mkdir -p "$OUT/lib" "$OUT/build"
 cp $PKG/*.py "$OUT/"
+# ONLY="pencil_kernel lap_kernel": recompile just those sources with DEFS and
+# take the others' objects from the main build ($PKG/build, `make` first) --
+# a knob that touches one kernel file then costs one compile, not five
 objs=()
 for f in $SRC/csrc/*.hip; do
-  o="$OUT/build/$(basename "${f%.hip}").o"
-  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function \
-    -DTSA_SRC_HASH="\"variant-$NAME\"" $DEFS -c "$f" -o "$o" &
+  b=$(basename "${f%.hip}")
+  o="$OUT/build/$b.o"
+  if [ -n "$ONLY" ] && ! echo " $ONLY " | grep -q " $b "; then
+    cp "$PKG/build/$b.o" "$o"
+  else
+    /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function \
+      -DTSA_SRC_HASH="\"variant-$NAME\"" $DEFS -c "$f" -o "$o" &
+  fi
   objs+=("$o")
 done
 wait

@@ -99,3 +99,44 @@ def test_single_cube_software_baseline(tsa, orc, synth):
     assert parity["mismatches"] == 0
     r = single[f"configs[2]: {L}^3"]
     assert r["cpu_ms"] == 3.0 and r["speedup"] == 6.0 and r["cpu_runs"] == 3
+
+
+def test_profile_window_is_the_timed_launches():
+    """roofline.frac is computed from the profiled child's per-dispatch trace
+    of the timed launches only: the batch kernel's
+    warm-up launches and the single cube's untimed first call are dropped."""
+    import bench
+    rows = []
+    did = 0
+
+    def add(name, ns):
+        nonlocal did
+        did += 1
+        rows.append({"Dispatch_Id": str(did), "Kernel_Name": name,
+                     "Start_Timestamp": str(1000 * did), "End_Timestamp": str(1000 * did + ns)})
+    add("__amd_rocclr_copyBuffer", 5)
+    for ns in (900, 800, 700):  # cold warm-ups
+        add("void tsa::pencil_kernel<2, 8, true, false, false, true>(unsigned char const*)", ns)
+    for ns in (500, 510, 490, 500):
+        add("void tsa::pencil_kernel<2, 8, true, false, false, true>(unsigned char const*)", ns)
+    for ns in (99, 30, 31, 29):
+        add("void tsa::lap_kernel<1, 4, true, false, false, false, false, false>(unsigned char const*)", ns)
+    out = bench.timed_dispatches(list(reversed(rows)), warmup=3, steps=4)
+    pk = out["pencil_kernel"]
+    assert pk["calls"] == 4 and pk["avg_ns"] == 500.0 and pk["median_ns"] == 500.0
+    assert pk["max_ns"] == 510.0 and pk["dispatch_ids"] == [5, 8]
+    assert pk["name"] == "void tsa::pencil_kernel<2, 8, true, false, false, true>"
+    lk = out["lap_kernel"]
+    assert lk["calls"] == 3 and lk["avg_ns"] == 30.0 and lk["dispatch_ids"] == [10, 12]
+
+
+def test_fallback_summary_flags_any_fallback():
+    import bench
+    clean = {"lap_timeouts": 0, "uncertified": 0, "invalid_scores": 0, "stable_vs_warmup": True}
+    one = {"lap_timeouts": 0, "uncertified": 0, "timed_calls": 5, "invalid_reps": 0, "scores_agree": True}
+    s = bench.fallback_summary(clean, {"a": {"fallbacks": one}, "b": {"error": "x"}})
+    assert s["all_zero"] is True and list(s["single_cube"]) == ["a"]
+    assert not bench.fallback_summary(clean, {"a": {"fallbacks": dict(one, invalid_reps=1)}})["all_zero"]
+    assert not bench.fallback_summary(dict(clean, lap_timeouts=1), {})["all_zero"]
+    assert not bench.fallback_summary(dict(clean, stable_vs_warmup=False), {})["all_zero"]
+    assert bench.split_devices(1) == "0,0" and bench.split_devices(4) == "0,1,2,3"

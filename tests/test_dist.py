@@ -103,6 +103,34 @@ def test_bench_spawn_world2_gloo(tsa, orc, per_gpu):
     assert rec["gathered"] == rec["oracle"] and len(rec["gathered"]) == 2 * per_gpu
 
 
+def test_bench_spawn_world8_record_fields(tsa, orc):
+    """The driver's N = 8 line: bench.py's spawn path with 8 gloo ranks (CPU
+    stand-in, tests/_bench_cpu_rank.py) prints one record whose
+    config.devices.dist_world_size is 8, whose split-over-devices leg is laid
+    over devices 0..7, and whose gathered scores equal the oracle's."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "_bench_cpu_rank.py"),
+                        "--gpus", "8", "--per-gpu", "1", "--length", "8",
+                        "--steps", "1", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 8 and rec["config"]["world_size"] == 8
+    assert rec["config"]["devices"]["dist_world_size"] == 8
+    assert rec["config"]["devices"]["backend"] == "gloo"
+    assert rec["config"]["split_devices"] == "0,1,2,3,4,5,6,7"
+    assert rec["gathered"] == rec["oracle"] and len(rec["gathered"]) == 8
+    assert rec["fallbacks"]["all_zero"] is True
+
+
 def test_bench_rejects_world_mismatch():
     import subprocess
     import sys

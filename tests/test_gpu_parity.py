@@ -377,6 +377,38 @@ def test_pencil_lap_streaming_batch(gpu, orc, monkeypatch, tmp_path):
     assert gpu.fallback_count() == before, "a lap hand-off timed out and was rescored"
 
 
+def test_lap_looped_rounds_several_per_cu(gpu, orc, monkeypatch):
+    """A looped multi-round lap grid at two or more workgroups per CU (ADVICE
+    r4): the residency estimate is load-bearing there -- a physical block that
+    only starts once the resident ones finish would leave its round-0
+    consumers spinning into a timeout and a counted rescore. Sync and async
+    paths: oracle-equal, no fallback counted, no TSA_SCORE_INVALID."""
+    monkeypatch.setenv("TSA_PENCIL_MODE", "lap")
+    monkeypatch.setenv("TSA_LAP_M", "1")
+    monkeypatch.setenv("TSA_LAP_NW", "4")
+    rng = np.random.default_rng(123)
+    triples = [tuple(rng.integers(0, 4, n).astype(np.uint8) for n in (64, 256, int(rng.integers(65, 129))))
+               for _ in range(24)]
+    plan = gpu.describe_plan(len(triples), 64, 256, 128, sync=True)
+    kv = dict(f.split("=") for f in plan.split() if "=" in f)
+    assert int(kv["waves"]) >= 2 and int(kv["wpc"]) >= 2, plan
+    seqs, offs = gpu.pack_batch(triples)
+    ref = orc.score_batch(seqs, offs, nthreads=8)
+    before = gpu.fallback_count()
+    assert np.array_equal(gpu.score_batch(triples), ref), plan
+    assert gpu.fallback_count() == before, "a lap hand-off timed out and was rescored: " + plan
+    import torch
+    d_seqs, d_offs = torch.from_numpy(seqs).cuda(), torch.from_numpy(offs).cuda()
+    d_sc = torch.zeros(len(triples), dtype=torch.int32, device="cuda")
+    p = gpu.TsaParams.default()
+    ws = gpu.workspace_size(len(triples), 64, 256, 128, p, "pencil")
+    d_ws = torch.empty(ws, dtype=torch.uint8, device="cuda")
+    gpu.score_batch_async(d_seqs.data_ptr(), d_offs.data_ptr(), len(triples), 64, 256, 128, d_sc.data_ptr(),
+                          d_ws.data_ptr(), ws, torch.cuda.current_stream().cuda_stream, p, "pencil")
+    torch.cuda.synchronize()
+    assert np.array_equal(d_sc.cpu().numpy(), ref), plan
+
+
 def test_pencil_ragged_batch(gpu, orc):
     rng = np.random.default_rng(77)
     triples = []
