@@ -489,12 +489,19 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 #ifndef TSA_LAP_WPE1
 #define TSA_LAP_WPE1 6
 #endif
+// The checked kernel's monitor: per-wave slots written with plain stores and
+// reduced per triple by lap_certify (1), or two same-address atomics per wave
+// (0, rounds 1-4). Thousands of waves of one cube contend for the two words,
+// and a looped workgroup waits for its atomics (vmcnt(0)) before its next lap.
+#ifndef TSA_CHK_SLOTS
+#define TSA_CHK_SLOTS 1
+#endif
 // wave 0 reads only the payload words of its tagged y record (ds_read2_b32):
 // a 16-byte read hands the compiler the two dead tag registers, which it
 // reuses before the read has landed -- a write-after-write wait that puts
 // the record read's latency in front of the pre-cell
-#ifndef TSA_LAP_Y2
-#define TSA_LAP_Y2 0
+#ifndef TSA_LAP_Y2  // (measured: 64^3 / 256^3 / 512^3 0.5-1 % faster, profiles/r5a_lap_y2_ab.jsonl)
+#define TSA_LAP_Y2 1
 #endif
 __host__ __device__ constexpr int lap_waves_per_eu(int M, bool lit = false, bool chk = false) {
   return lit ? (M == 1 ? 4 : 3) : M == 1 ? (chk ? 4 : TSA_LAP_WPE1) : M == 2 ? (chk ? TSA_LAP_WPE2C : TSA_LAP_WPE2) : 2;
@@ -514,8 +521,8 @@ __device__ __forceinline__ void static_for(F &&f) {
   } while (0)
 
 // CHK (int16 form only): the checked kernel -- every real cell's best is
-// folded into a per-lane max / min; each wave's extremes go to mon[tri]
-// (max) and mon[n + tri] (min) by atomics, and lap_certify() decides whether
+// folded into a per-lane max / min; each wave's extremes go to its own monitor
+// slots (TSA_CHK_SLOTS), and lap_certify() reduces a triple's and decides whether
 // any candidate of the literal RTL recurrence could have wrapped.
 // A launch runs laps [L0, L1) of the cube (a single launch: [0, G)). SYS: one
 // part of a cube split over devices (lap_launch_split) -- every hand-off load
@@ -1409,9 +1416,15 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
         mn = min(mn, __shfl_xor(mn, d));
       }
       if (lane == 0) {
-        const int32_t ntri = NC / GZ;
-        atomicMax(mon + tri, mx);
-        atomicMin(mon + ntri + tri, mn);
+        if constexpr (TSA_CHK_SLOTS) {  // this wave's slot of [max] NC G NW, [min] NC G NW
+          const int64_t nslot = (int64_t)NC * G * NW;
+          mon[lid * NW + w] = mx;
+          mon[nslot + lid * NW + w] = mn;
+        } else {
+          const int32_t ntri = NC / GZ;
+          atomicMax(mon + tri, mx);
+          atomicMin(mon + ntri + tri, mn);
+        }
       }
     }
 #if defined(TSA_DIAG)
@@ -1466,14 +1479,44 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
   }
 }
 
-// Certification of the checked kernel's triples (one thread each): a score
-// stands when every best it saw lies in [best_min, best_max].
-__global__ __launch_bounds__(256) void lap_certify(const int32_t *__restrict__ mon, int32_t n,
-                                                   CheckLimits lim, int32_t *__restrict__ scores) {
-  const int32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  if (mon[i] > lim.best_max || mon[n + i] < lim.best_min) {
-    if (scores[i] != TSA_SCORE_INVALID) scores[i] = TSA_SCORE_UNCERTIFIED;
+// Certification of the checked kernel's triples: a score stands when every
+// best it saw lies in [best_min, best_max]. TSA_CHK_SLOTS: one workgroup per
+// triple reduces its per_tri wave slots ([max] at mon, [min] at mon + nslot;
+// slots of waves that did not run keep the launch's neutral fill); otherwise
+// one thread per triple reads its two atomic words.
+__global__ __launch_bounds__(256) void lap_certify(const int32_t *__restrict__ mon, int32_t n, int64_t nslot,
+                                                   int32_t per_tri, CheckLimits lim, int32_t *__restrict__ scores) {
+  if constexpr (TSA_CHK_SLOTS) {
+    __shared__ int32_t red[2][4];
+    const int32_t i = blockIdx.x;
+    const int64_t base = (int64_t)i * per_tri;
+    int32_t mx = INT32_MIN, mn = INT32_MAX;
+    for (int32_t j = threadIdx.x; j < per_tri; j += 256) {
+      mx = max(mx, mon[base + j]);
+      mn = min(mn, mon[nslot + base + j]);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      mx = max(mx, __shfl_xor(mx, d));
+      mn = min(mn, __shfl_xor(mn, d));
+    }
+    if ((threadIdx.x & 63) == 0) {
+      red[0][threadIdx.x >> 6] = mx;
+      red[1][threadIdx.x >> 6] = mn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      mx = max(max(red[0][0], red[0][1]), max(red[0][2], red[0][3]));
+      mn = min(min(red[1][0], red[1][1]), min(red[1][2], red[1][3]));
+      if ((mx > lim.best_max || mn < lim.best_min) && scores[i] != TSA_SCORE_INVALID)
+        scores[i] = TSA_SCORE_UNCERTIFIED;
+    }
+  } else {
+    const int32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    if (mon[i] > lim.best_max || mon[n + i] < lim.best_min) {
+      if (scores[i] != TSA_SCORE_INVALID) scores[i] = TSA_SCORE_UNCERTIFIED;
+    }
   }
 }
 
@@ -1652,7 +1695,10 @@ LapGeom lap_geom(int32_t n, int32_t max_la, int32_t max_lb, int32_t max_lc, int 
   g.YRB = g.ZRB = pow2(T);
   g.blocks = (int64_t)g.G * g.CH * 8;
   // progress words, the error word (+63 spare), the checked kernel's monitor (2 n)
-  g.prog_bytes = (((size_t)wgs * LAP_PROG_STRIDE + 64 + 2 * (size_t)n) * sizeof(int32_t) + 255) &
+  // progress words, the error word (+63 spare), the checked kernel's monitor
+  // (TSA_CHK_SLOTS: two words per compute wave; else two per triple)
+  const size_t mon_words = TSA_CHK_SLOTS ? 2 * (size_t)wgs * NW : 2 * (size_t)n;
+  g.prog_bytes = (((size_t)wgs * LAP_PROG_STRIDE + 64 + mon_words) * sizeof(int32_t) + 255) &
                  ~(size_t)255;
   g.yf_bytes = (size_t)wgs * g.YR * M * 1024;
   g.zf_bytes = (size_t)wgs * g.ZR * NW * LAP_ZREC_WAVE;
@@ -1787,9 +1833,12 @@ static int launch_lap_fn(LapKernelFn kfn, int NW, const uint8_t *d_seqs, const i
     return TSA_EINTERNAL;  // a chunk's regions must fit the batch's
   int32_t *prog = (int32_t *)d_ws;
   uint32_t *err = lap_err_word(ga, n, d_ws);
-  int32_t *mon = chk ? (int32_t *)err + 64 : aux;  // [max(best)] n, [min(best)] n
-  if (chk && (hipMemsetAsync(mon, 0x80, (size_t)n * 4, stream) != hipSuccess ||
-              hipMemsetAsync(mon + n, 0x7F, (size_t)n * 4, stream) != hipSuccess))
+  // [max(best)] nslot, [min(best)] nslot: one slot per compute wave of this
+  // launch (TSA_CHK_SLOTS), else per triple; neutral fill for waves that do not run
+  int32_t *mon = chk ? (int32_t *)err + 64 : aux;
+  const int64_t nslot = TSA_CHK_SLOTS ? (int64_t)g.NC * g.G * NW : (int64_t)n;
+  if (chk && (hipMemsetAsync(mon, 0x80, (size_t)nslot * 4, stream) != hipSuccess ||
+              hipMemsetAsync(mon + nslot, 0x7F, (size_t)nslot * 4, stream) != hipSuccess))
     return TSA_EDEVICE;
   uint8_t *yf = (uint8_t *)d_ws + ga.prog_bytes;
   uint8_t *zf = yf + ga.yf_bytes;
@@ -1809,8 +1858,8 @@ static int launch_lap_fn(LapKernelFn kfn, int NW, const uint8_t *d_seqs, const i
       }) != hipSuccess)
     return TSA_EDEVICE;
   if (chk) {
-    hipLaunchKernelGGL(lap_certify, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, stream, mon, n,
-                       *chk, d_scores);
+    hipLaunchKernelGGL(lap_certify, dim3((uint32_t)(TSA_CHK_SLOTS ? n : (n + 255) / 256)), dim3(256), 0, stream,
+                       mon, n, nslot, (int32_t)(g.G * g.GZ * NW), *chk, d_scores);
   }
   if (hipGetLastError() != hipSuccess) return TSA_EDEVICE;
   if (trace) {

@@ -56,6 +56,38 @@ __host__ __device__ constexpr int helix_pd(int M) { return M >= 8 ? 2 : M >= 4 ?
 // skew and record slots per wave; M >= 4 keeps skew 1 (twice the slots would not fit LDS)
 __host__ __device__ constexpr int helix_skew(int M) { return M <= 2 ? TSA_SKEW : 1; }
 constexpr int RING_EXTRA = 8;
+// V-space M = 2: the lap period P is a multiple of 4, so each wave meets its
+// half-mask / lap-wrap events (xpos0 = 64M, 128M, P) at one static step of the
+// four-step group (xpos0 is -2w mod 4 at the group start); the other three
+// steps advance with no compare and no branch
+#ifndef TSA_EV_STATIC
+#define TSA_EV_STATIC 1
+#endif
+// V-space: the face values H(s) = lam q kept as wave-uniform integers and
+// encoded to f16 bits in SALU (f16x2_int), so they live in SGPRs: no VALU add
+// per step, and the bfi / perm that inject them read the SGPR directly
+#ifndef TSA_H_SALU
+#define TSA_H_SALU 1
+#endif
+// f16 bits of the integer v in both halves, exact for 0 <= v <= 2047 --
+// integer ops only, so a wave-uniform v stays in SALU (~8 instructions). The
+// face values lam q are >= 0, and < 2048 at every real cell (use_vs); a
+// padding position (x > LA) may see a larger q, clamped to a finite value
+// (its cells feed only padding cells and the x = 1 inputs the bfi replaces).
+// With c = clz(v), v << (c - 21) puts the leading 1 at bit 10, which adds the
+// one missing from the exponent field (45 - c - 1) + 1 = e + 15.
+__device__ __forceinline__ uint32_t f16x2_int(int32_t v) {
+  const uint32_t a = (uint32_t)min(max(v, 0), 2047);
+  const uint32_t c = (uint32_t)__builtin_clz(a | 1u);
+  const uint32_t h = a == 0 ? 0u : (a << (c - 21u)) + ((45u - c) << 10);
+  return h | (h << 16);
+}
+// v_bfi_b32 with an SGPR source for the selected bits
+__device__ __forceinline__ uint32_t vbfi_s(uint32_t mask, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mask), "s"(a), "v"(b));
+  return r;
+}
 // Ablation knobs (timing diagnostics only: the scores are WRONG when set):
 // TSA_ABL_ZOWN / TSA_ABL_ZREC replace the DPP + v_perm z-shift of the own
 // (Iz, Ixz) / the row-above (Iyz, M) messages by register moves, TSA_ABL_INJ
@@ -105,6 +137,7 @@ static PencilGeom pencil_geom(int32_t max_la, int32_t max_lc) {
   g.two = helix_two(max_lc);
   g.P = std::max(max_la, g.two ? 64 : 128 * g.M);
   g.P = (g.P + g.M - 1) / g.M * g.M;  // even for M = 2: the x = 1 register is PH ^ (w & 1)
+  if (g.M == 2 && !g.two && TSA_EV_STATIC) g.P = (g.P + 3) / 4 * 4;  // TSA_EV_STATIC
   g.R = g.P + RING_EXTRA;
   g.ring_bytes_per_triple = (int64_t)g.R * g.M * 64 * REC_BYTES;
   return g;
@@ -409,17 +442,22 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     // 1-based) -- the x = 0 face at the x = 1 position and, one and two steps
     // ahead, the z = 0 face of position 0; one v_pk_add per step, reset at a wrap
     uint32_t Hr[4] = {0u, 0u, 0u, 0u};
-    auto h_at = [&](int32_t s) -> uint32_t {
+    int32_t Hq[4] = {0, 0, 0, 0};  // TSA_H_SALU: lam q as integers (Hr = their f16 bits)
+    auto hq_at = [&](int32_t s) -> int32_t {
       const int32_t u = s - HSK * w;
       const int32_t lp = u >= 0 ? u / P : -((P - 1 - u) / P);
-      return h_bits(pa.lam * (lp * NW + w + 1 + (u - lp * P)));
+      return pa.lam * (lp * NW + w + 1 + (u - lp * P));
     };
+    auto h_at = [&](int32_t s) -> uint32_t { return TSA_H_SALU ? f16x2_int(hq_at(s)) : h_bits(hq_at(s)); };
     if constexpr (VS) {
+      Hq[0] = hq_at(0);
+      Hq[1] = hq_at(1);
+      Hq[3] = Hq[0] - pa.lam;
       Hr[0] = h_at(0);
       Hr[1] = h_at(1);
       // the step-0 injection's (0, y-1, z-1) face is H(0) - lam (wave 0 starts
       // its first row at step 0 with no wrap that would have set it)
-      Hr[3] = U(H(Hr[0]) - H(pa.v_lam));
+      Hr[3] = TSA_H_SALU ? f16x2_int(Hq[3]) : U(H(Hr[0]) - H(pa.v_lam));
       if (w == 0) {  // position 0's z = 0 faces at steps 0 and 1 (as if shifted in at steps -1, -2)
 #pragma unroll
         for (int i = 0; i < M; ++i) {
@@ -525,10 +563,17 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
         for (int i = 0; i < M; ++i) {
           if (ISC >= 0 ? i == ISC : i == is) {
             if constexpr (VS) {  // faces (0,y,z), (0,y-1,z), (0,y,z-1): lam(y+z-1); (0,y-1,z-1): one lam less
-              inIx[i] = vbfi(m1, Hr[PQ & 3], inIx[i]);
-              inIxy[i] = vbfi(m1, Hr[PQ & 3], inIxy[i]);
-              inIxz[i] = vbfi(m1, Hr[PQ & 3], inIxz[i]);
-              inM[i] = vbfi(m1, Hr[(PQ + 3) & 3], inM[i]);
+              if constexpr (TSA_H_SALU) {
+                inIx[i] = vbfi_s(m1, Hr[PQ & 3], inIx[i]);
+                inIxy[i] = vbfi_s(m1, Hr[PQ & 3], inIxy[i]);
+                inIxz[i] = vbfi_s(m1, Hr[PQ & 3], inIxz[i]);
+                inM[i] = vbfi_s(m1, Hr[(PQ + 3) & 3], inM[i]);
+              } else {
+                inIx[i] = vbfi(m1, Hr[PQ & 3], inIx[i]);
+                inIxy[i] = vbfi(m1, Hr[PQ & 3], inIxy[i]);
+                inIxz[i] = vbfi(m1, Hr[PQ & 3], inIxz[i]);
+                inM[i] = vbfi(m1, Hr[(PQ + 3) & 3], inM[i]);
+              }
             } else {
               inIx[i] = vbfi(m1, fsv, inIx[i]);
               inIxy[i] = vbfi(m1, fpv, inIxy[i]);
@@ -631,8 +676,15 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #pragma unroll
       for (int i = 0; i < M; ++i) { rz[i] = rec[i].z; rw[i] = rec[i].w; }
       // position 0 advances to u0 + 1
+      // (TSA_EV_STATIC: the events fall on step (2w - 1) mod 4 of a group only)
+      constexpr bool EV_SKIP = VS && M == 2 && TSA_EV_STATIC && HSK == 2 && WPAR >= 0 && PQ >= 0 && PQ < 4 &&
+                               (PQ & 3) != (WPAR == 0 ? 3 : 1);
       auto advance = [&]() {
 #if TSA_HM_TRACK
+        if constexpr (EV_SKIP) {
+          ++xpos0;
+          return;
+        }
         if (__builtin_expect(++xpos0 == next_ev, 0)) {
           if (xpos0 == P) {
             xpos0 = 0;
@@ -640,9 +692,18 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
             row_terms();
             if constexpr (VS) {  // a new row at position 0: H(t .. t+2) restart
               const int32_t y = lap0 * NW + w + 1;
-              Hr[PQ & 3] = h_bits(pa.lam * (y - 1));
-              Hr[(PQ + 1) & 3] = h_bits(pa.lam * y);
-              Hr[(PQ + 2) & 3] = h_bits(pa.lam * (y + 1));
+              if constexpr (TSA_H_SALU) {
+                Hq[PQ & 3] = pa.lam * (y - 1);
+                Hq[(PQ + 1) & 3] = pa.lam * y;
+                Hq[(PQ + 2) & 3] = pa.lam * (y + 1);
+                Hr[PQ & 3] = f16x2_int(Hq[PQ & 3]);
+                Hr[(PQ + 1) & 3] = f16x2_int(Hq[(PQ + 1) & 3]);
+                Hr[(PQ + 2) & 3] = f16x2_int(Hq[(PQ + 2) & 3]);
+              } else {
+                Hr[PQ & 3] = h_bits(pa.lam * (y - 1));
+                Hr[(PQ + 1) & 3] = h_bits(pa.lam * y);
+                Hr[(PQ + 2) & 3] = h_bits(pa.lam * (y + 1));
+              }
             }
           }
           hmCur = hm_of(xpos0);
@@ -658,7 +719,12 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
 #endif
       };
       if constexpr (VS) {
-        Hr[(PQ + 2) & 3] = U(H(Hr[(PQ + 1) & 3]) + H(pa.v_lam));
+        if constexpr (TSA_H_SALU) {
+          Hq[(PQ + 2) & 3] = Hq[(PQ + 1) & 3] + pa.lam;
+          Hr[(PQ + 2) & 3] = f16x2_int(Hq[(PQ + 2) & 3]);
+        } else {
+          Hr[(PQ + 2) & 3] = U(H(Hr[(PQ + 1) & 3]) + H(pa.v_lam));
+        }
         advance();
         // z = 0 faces of position 0: (x, y, 0) and (x, y-1, 0) at step t+1,
         // (x-1, y, 0) and (x-1, y-1, 0) at step t+2

@@ -129,8 +129,10 @@ def test_describe_plan(tsa):
     finally:
         del os.environ["TSA_PENCIL_MODE"]
         os.environ.pop("TSA_LAP_CHUNK", None)
-    # M = 2 lap periods are even (the x = 1 register is then PH ^ (w & 1))
-    assert "M=2 NW=8 P=258" in tsa.describe_plan(512, 257, 40, 255, p)
+    # M = 2 lap periods are multiples of 4: even (the x = 1 register is then
+    # PH ^ (w & 1)), and each wave's lap-wrap events fall on one static step of
+    # the four-step group (TSA_EV_STATIC)
+    assert "M=2 NW=8 P=260" in tsa.describe_plan(512, 257, 40, 255, p)
     assert "M=2 NW=8 P=256" in tsa.describe_plan(512, 255, 40, 255, p)
     p16 = tsa.TsaParams.default(score_bits=16)
     assert tsa.describe_plan(1, 1024, 1024, 1024, p16).startswith("pencil lap i16 rtl")

@@ -42,6 +42,8 @@ def emulate(triples, match=1, mismatch=-1, go=2, ge=1, sop=False, vs=False):
     KS = 64 if two else 128 * M
     P = max(max_la, 64 if two else 128 * M)
     P = -(-P // M) * M
+    if M == 2 and not two:  # the kernel's TSA_EV_STATIC: P a multiple of 4
+        P = -(-P // 4) * 4
     R = P + RING_EXTRA
     lam = ge if vs else 0
     assert not vs or ge == -mismatch
