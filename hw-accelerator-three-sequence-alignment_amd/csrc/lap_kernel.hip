@@ -496,6 +496,12 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 #ifndef TSA_CHK_SLOTS
 #define TSA_CHK_SLOTS 1
 #endif
+// Lean step: the producer's progress word read every step (no poll flag kept
+// in a VGPR across the pre-cell, no conditional read), and the next A codes
+// at a constant offset from a base set once per step pair
+#ifndef TSA_LAP_LEAN
+#define TSA_LAP_LEAN 1
+#endif
 // wave 0 reads only the payload words of its tagged y record (ds_read2_b32):
 // a 16-byte read hands the compiler the two dead tag registers, which it
 // reuses before the read has landed -- a write-after-write wait that puts
@@ -1072,6 +1078,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
     const int32_t zstride = (zin || FACES) ? ZREC : 0;
     uint32_t a_nx[M];
     load_a<M>(a_lane, a_nx);
+    uint32_t a_pair = a_lane;  // TSA_LAP_LEAN: a_lane's entry of the step pair's first step
     // producer side: my consumers' progress (y: the lap below, via the last
     // wave; z: the tile to the right, every wave), LDS-DMA'd by the loader
     int32_t seen_in = 0, seen_out = 0, seen_y = 0, seen_z = 0;
@@ -1114,7 +1121,8 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
       uint32_t a[M];
 #pragma unroll
       for (int i = 0; i < M; ++i) a[i] = a_nx[i];
-      load_a<M>(a_lane + 4u * (uint32_t)(t + 1), a_nx);
+      if constexpr (TSA_LAP_LEAN) load_a_off<M>(a_pair, PH + 1, a_nx);  // entry t + 1 of a_lane's table
+      else load_a<M>(a_lane + 4u * (uint32_t)(t + 1), a_nx);
       // ---- input reads, issued first: the producer's progress word (unless the
       // cached value covers step t), then its record. LDS executes a wave's DS
       // instructions in order, so a word read that covers t proves the record
@@ -1125,7 +1133,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
       const int32_t need = ROLE == 0 ? t + 1 : t;
       const int32_t *const pword = ROLE == 0 ? pw + 64 * NW : pw + 64 * (w - 1);
       const bool waits = ROLE != 0 || yin || zin || FACES;
-      const bool poll = waits && seen_in < need;
+      const bool poll = TSA_LAP_LEAN ? waits : (waits && seen_in < need);
       int32_t fl_v = 0;
       if (poll)
         fl_v = *(volatile const __attribute__((address_space(3))) int32_t *)(
@@ -1378,9 +1386,11 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
       constexpr std::true_type last{};
 #pragma unroll 1
       for (; t + 1 < T1; t += 2) {
+        a_pair = a_lane + 4u * (uint32_t)t;
         LAP_INLINE(step(P0, role, t, mid));
         LAP_INLINE(step(P1, role, t + 1, mid));
       }
+      a_pair = a_lane + 4u * (uint32_t)t;
       if (t < T1) {
         LAP_INLINE(step(P0, role, t, mid));
         LAP_INLINE(step(P1, role, t + 1, last));

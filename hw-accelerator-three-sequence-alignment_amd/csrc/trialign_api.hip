@@ -587,6 +587,22 @@ int tsa_score_gpu_multi(const uint8_t *a, int32_t la, const uint8_t *b, int32_t 
                std::chrono::steady_clock::now().time_since_epoch()).count() * 1e-3;
   };
   for (int i = 0; i < np; ++i) parts[i] = LapPart{devices[i], nullptr, 0, 0, nullptr, nullptr, nullptr};
+  // Parts sharing a device run concurrently, each on its own stream, when all
+  // their workgroups fit on that device at once (every lap resident: no part's
+  // workgroups can hold the CU slots an earlier part's undispatched ones need);
+  // otherwise one after another on one stream (below).
+  bool concurrent = g.per_cu > 0;
+  for (int i = 0; i < np && concurrent; ++i) {
+    int64_t blocks = 0;
+    for (int j = 0; j < np; ++j)
+      if (devices[j] == devices[i])
+        blocks += ((int64_t)g.G * (j + 1) / np - (int64_t)g.G * j / np) * g.CH * 8;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, devices[i]) != hipSuccess || cus <= 0 ||
+        blocks > (int64_t)cus * g.per_cu)
+      concurrent = false;
+  }
+  if (const char *e = getenv("TSA_SPLIT_SERIAL")) concurrent = concurrent && atoi(e) == 0;  // A/B knob
   // peer access between the distinct devices (each part writes into its
   // neighbours' workspaces, every part into the last one's error word)
   for (int i = 0; i < np; ++i)
@@ -605,12 +621,13 @@ int tsa_score_gpu_multi(const uint8_t *a, int32_t la, const uint8_t *b, int32_t 
     q.L0 = (int32_t)((int64_t)g.G * i / np);
     q.L1 = (int32_t)((int64_t)g.G * (i + 1) / np);
     HIPCHK(hipSetDevice(q.device));
-    // parts sharing a device run one after another on the first one's stream:
-    // launched concurrently, a later part's workgroups can take the CU slots
-    // an earlier part's undispatched workgroups need, and wait on them (two
-    // 256-workgroup parts of 1024^3 at one workgroup per CU timed out). In lap
-    // order with full-length rings an earlier part never waits on a later one.
-    for (int j = 0; j < i && !q.stream; ++j)
+    // unless every part fits at once (concurrent), parts sharing a device run
+    // one after another on the first one's stream: launched concurrently, a
+    // later part's workgroups can take the CU slots an earlier part's
+    // undispatched workgroups need, and wait on them (two 256-workgroup parts
+    // of 1024^3 at one workgroup per CU timed out). In lap order with
+    // full-length rings an earlier part never waits on a later one.
+    for (int j = 0; j < i && !q.stream && !concurrent; ++j)
       if (parts[j].device == q.device) q.stream = parts[j].stream;
     own[i] = q.stream == nullptr;
     if (own[i]) HIPCHK(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));

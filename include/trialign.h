@@ -186,8 +186,11 @@ int tsa_pack2(const uint8_t *syms, int64_t n, uint8_t *out);
  * n_devices contiguous runs, part i on devices[i]; the last lap of part i
  * hands its y records to part i+1 by system-scope stores into part i+1's
  * fine-grained workspace over xGMI (peer access is enabled between the listed
- * devices). A device may be listed more than once: its parts then run one
- * after another on one stream of that device. The factored arithmetic where
+ * devices). A device may be listed more than once: its parts then run
+ * concurrently on streams of their own when all their workgroups fit on the
+ * device at once, else one after another on one stream of that device (a
+ * part that waited for CU slots held by a later part could never finish).
+ * The factored arithmetic where
  * it is exact a priori, else the RTL's literal wrapped arithmetic (any
  * parameter set); TSA_ERANGE with fewer laps than n_devices (or no lap
  * schedule). A timed-out hand-off returns TSA_EINTERNAL (never a silent

@@ -2,8 +2,10 @@
 8(f)2) against the same cube as one part, and print one JSON object.
 
 bench.py runs this as a child process (a fault here cannot take the bench
-line down): on one GPU the parts share device 0 (run one after another on
-one stream -- the hand-off protocol without the xGMI hop); under the driver's
+line down): on one GPU the parts share device 0 (concurrently, on streams of
+their own, when all their workgroups fit at once -- the 256^3 case; else one
+after another on one stream, as 1024^3: the hand-off protocol without the
+xGMI hop); under the driver's
 N-GPU run rank 0 passes devices 0..N-1 (the real multi-GPU split). A case
 that fails records {"error": ...} in place of its score.
 
