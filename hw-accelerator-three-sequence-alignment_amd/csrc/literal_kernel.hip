@@ -32,6 +32,13 @@
 namespace tsa {
 
 constexpr int LIT_NW = 8, LIT_S = 2, LIT_RING_EXTRA = 8;
+// M <= 2: P a multiple of 4, so (as in the pencil helix, TSA_EV_STATIC) each
+// wave meets the x' = 0 half-mask and lap-wrap events at one static step of
+// its four-step group, the x' = 0 register is the step's parity (M = 2), and
+// the injection is a tracked mask with no per-step branch
+#ifndef TSA_LIT_STATIC
+#define TSA_LIT_STATIC 1
+#endif
 // ring rows wave 0 prefetches (LDS-DMA): 8, 4 at M = 4 (LDS)
 __host__ __device__ constexpr int lit_pd(int M) { return M >= 4 ? 4 : 8; }
 
@@ -45,6 +52,7 @@ static LitGeom lit_geom(int32_t max_la, int32_t max_lb, int32_t max_lc) {
   g.M = max_lc <= 128 ? 1 : max_lc <= 256 ? 2 : 4;
   g.P = std::max(max_la + 1, 128 * g.M);  // x' = 0 .. LA: the face column first
   g.P = (g.P + g.M - 1) / g.M * g.M;       // M = 2: the x' = 0 register is (t - w) parity
+  if (g.M <= 2 && TSA_LIT_STATIC) g.P = (g.P + 3) / 4 * 4;  // TSA_LIT_STATIC
   g.R = g.P + LIT_RING_EXTRA;
   g.ring_bytes_per_triple = (int64_t)g.R * g.M * 64 * REC_BYTES;
   g.lds = (size_t)(LIT_NW - 1) * 2 * LIT_S * g.M * 1024 + (size_t)lit_pd(g.M) * g.M * 1024 +
@@ -276,6 +284,15 @@ __global__ __launch_bounds__(64 * LIT_NW) void literal_kernel(
     }
     int32_t xpos0 = (P - ((S * w) % P)) % P;  // position at x' = 0 at step t
     int32_t lap0 = w == 0 ? 0 : -1;
+    // TSA_LIT_STATIC: the x' = 0 half mask (low below 64M, high below ZT, none
+    // from ZT to the wrap), switched at those events
+    constexpr bool LSTAT = TSA_LIT_STATIC && M <= 2;
+    auto hm_of = [&](int32_t xp) -> uint32_t {
+      return xp >= ZT ? 0u : xp >= 64 * M ? 0xFFFF0000u : 0x0000FFFFu;
+    };
+    auto ev_of = [&](int32_t xp) -> int32_t { return xp < 64 * M ? 64 * M : xp < ZT ? ZT : P; };
+    uint32_t hmCur = hm_of(xpos0);
+    int32_t next_ev = ev_of(xpos0);
     auto bcode = [&](int32_t row) -> uint32_t { return (row >= 0 && row < lb) ? sB[row] : 0u; };
     uint32_t binj = bcode(lap0 * NW + w + 1);  // b_{y+1} of the row that starts at x' = 0
     uint32_t bcur = bcode(lap0 * NW + w);      // b_y of position 0's row (the z = 0 face)
@@ -314,7 +331,12 @@ __global__ __launch_bounds__(64 * LIT_NW) void literal_kernel(
     auto step = [&](auto ph, auto role, int32_t t) {
       constexpr int Q = decltype(ph)::value;  // t & 3
       constexpr int PH = Q & 1;
-      constexpr int ROLE = decltype(role)::value;
+      constexpr int ROLE = decltype(role)::value & 3;
+      constexpr int WPAR = (decltype(role)::value >> 2) - 1;  // wave parity (-1: unknown)
+      // LSTAT: the x' = 0 register is (t - 2w) mod M = PH (P even); the events
+      // fall on step (2w - 1) mod 4 of the group only
+      constexpr int IS = M == 1 ? 0 : (LSTAT && M == 2) ? PH : -1;
+      constexpr bool EV_HERE = !LSTAT || WPAR < 0 || Q == (WPAR == 0 ? 3 : 1);
       uint32_t a[M];
 #pragma unroll
       for (int i = 0; i < M; ++i) a[i] = a_nx[i];
@@ -342,15 +364,15 @@ __global__ __launch_bounds__(64 * LIT_NW) void literal_kernel(
       }
       // ---- x' = 0 at position xpos0: the face column (all 7 inputs 0) and the
       // next row's B code for its successors
-      if (xpos0 < ZT) {
+      if (LSTAT || xpos0 < ZT) {  // (LSTAT: hmCur is 0 past ZT)
         int32_t ls, is, hs;
         pos_split<M>(xpos0, ls, is, hs);
-        const uint32_t hm = hs ? 0xFFFF0000u : 0x0000FFFFu;
+        const uint32_t hm = LSTAT ? hmCur : hs ? 0xFFFF0000u : 0x0000FFFFu;
         uint32_t m1;
         asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(m1) : "v"(hm), "s"(1ull << ls));
 #pragma unroll
         for (int i = 0; i < M; ++i) {
-          if (i == is) {
+          if (IS >= 0 ? i == IS : i == is) {
             X[i] = vbfi(m1, zero, X[i]);
             Y[i] = vbfi(m1, zero, Y[i]);
             Z[i] = vbfi(m1, zero, Z[i]);
@@ -416,7 +438,20 @@ __global__ __launch_bounds__(64 * LIT_NW) void literal_kernel(
         oIx[i] = nIx[i];
         svIxy[i] = rec[i].y;
       }
-      if (++xpos0 == P) {
+      if constexpr (LSTAT) {
+        if constexpr (!EV_HERE) {
+          ++xpos0;
+        } else if (__builtin_expect(++xpos0 == next_ev, 0)) {
+          if (xpos0 == P) {
+            xpos0 = 0;
+            ++lap0;
+            binj = bcode(lap0 * NW + w + 1);
+            bcur = bcode(lap0 * NW + w);
+          }
+          hmCur = hm_of(xpos0);
+          next_ev = ev_of(xpos0);
+        }
+      } else if (++xpos0 == P) {
         xpos0 = 0;
         ++lap0;
         binj = bcode(lap0 * NW + w + 1);
@@ -458,9 +493,12 @@ __global__ __launch_bounds__(64 * LIT_NW) void literal_kernel(
         step(Q3, role, t + 3);
       }
     };
-    if (w == 0) run(std::integral_constant<int, 0>{});
-    else if (w == NW - 1) run(std::integral_constant<int, 2>{});
-    else run(std::integral_constant<int, 1>{});
+    // role | (wave parity + 1) << 2 (LSTAT's static event step); NW is even
+    static_assert(NW % 2 == 0, "the last wave is odd");
+    if (w == 0) run(std::integral_constant<int, 0 + 4>{});
+    else if (w == NW - 1) run(std::integral_constant<int, 2 + 8>{});
+    else if (w & 1) run(std::integral_constant<int, 1 + 8>{});
+    else run(std::integral_constant<int, 1 + 4>{});
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x < 7) {  // unshift the final cell's states

@@ -2,7 +2,8 @@
 # Same-box A/B of variant libraries (scripts/build_variant.sh -> variants/<name>):
 # single cubes (spin preload) over PKGS, then the helix batch over HPKGS.
 # KERNEL (pencil) and BITS (12) select the single cubes' kernel and words
-# (e.g. KERNEL=checked LENS=1024 for the checked 1024^3 form).
+# (e.g. KERNEL=checked LENS=1024 for the checked 1024^3 form); HKERNEL the
+# batch's (plane: the literal helix).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=${TAG:-ab}; O=gpurun_out/$TAG; mkdir -p $O
@@ -15,7 +16,7 @@ for i in 1 2; do
   done
   for pk in $HPKGS; do
     echo "== helix $pk" >> $O/helix_ab.jsonl
-    TSA_PKG_DIR=$GRAFT_REPO_ROOT/$pk timeout -k 10 120 python tools/bench_variants.py --n 512 --L 256 --rounds 5 --variants "TSA_NONE=0" >> $O/helix_ab.jsonl 2>> $O/helix_ab.err || exit 1
+    TSA_PKG_DIR=$GRAFT_REPO_ROOT/$pk timeout -k 10 120 python tools/bench_variants.py --n 512 --L 256 --rounds 5 --kernel ${HKERNEL:-pencil} --variants "TSA_NONE=0" >> $O/helix_ab.jsonl 2>> $O/helix_ab.err || exit 1
   done
 done
 cat $O/single_ab.jsonl; [ -z "$HPKGS" ] || cat $O/helix_ab.jsonl

@@ -48,6 +48,8 @@ def emulate(a, b, c, match=1, mismatch=-1, go=2, ge=1, sop=False, bits=12):
     KS = 128 * M
     P = max(la + 1, KS)
     P = -(-P // M) * M
+    if M <= 2:  # the kernel's TSA_LIT_STATIC: P a multiple of 4
+        P = -(-P // 4) * 4
     R = P + RING_EXTRA
     Pen = penalties(go, ge)
 
