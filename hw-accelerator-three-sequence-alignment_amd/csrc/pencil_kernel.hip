@@ -69,6 +69,12 @@ constexpr int RING_EXTRA = 8;
 #ifndef TSA_H_SALU
 #define TSA_H_SALU 1
 #endif
+// V-space: step s's x = 1 injection applied to the state registers at the end
+// of step s - 1 (before the step barrier), not to the inputs at the start of
+// step s, where it stood between the barrier and the cell
+#ifndef TSA_PREINJ
+#define TSA_PREINJ 1
+#endif
 // f16 bits of the integer v in both halves, exact for 0 <= v <= 2047 --
 // integer ops only, so a wave-uniform v stays in SALU (~8 instructions). The
 // face values lam q are >= 0, and < 2048 at every real cell (use_vs); a
@@ -76,11 +82,25 @@ constexpr int RING_EXTRA = 8;
 // (its cells feed only padding cells and the x = 1 inputs the bfi replaces).
 // With c = clz(v), v << (c - 21) puts the leading 1 at bit 10, which adds the
 // one missing from the exponent field (45 - c - 1) + 1 = e + 15.
+// Written in SALU asm: left to itself the compiler picks v_med3_i32 for the
+// clamp and then keeps the whole encode in VALU (v is wave-uniform).
 __device__ __forceinline__ uint32_t f16x2_int(int32_t v) {
-  const uint32_t a = (uint32_t)min(max(v, 0), 2047);
-  const uint32_t c = (uint32_t)__builtin_clz(a | 1u);
-  const uint32_t h = a == 0 ? 0u : (a << (c - 21u)) + ((45u - c) << 10);
-  return h | (h << 16);
+  uint32_t r, a, c, t;
+  asm("s_min_u32 %1, %4, 0x7ff\n\t"       // a = min(v, 2047) (v >= 0; unsigned: a negative v clamps too)
+      "s_or_b32 %2, %1, 1\n\t"
+      "s_flbit_i32_b32 %2, %2\n\t"         // c = clz(a | 1), 21..31
+      "s_sub_u32 %3, %2, 21\n\t"
+      "s_lshl_b32 %3, %1, %3\n\t"          // a << (c - 21): the leading 1 at bit 10
+      "s_sub_u32 %2, 45, %2\n\t"
+      "s_lshl_b32 %2, %2, 10\n\t"
+      "s_add_u32 %3, %3, %2\n\t"           // + (45 - c) << 10
+      "s_cmp_eq_u32 %1, 0\n\t"
+      "s_cselect_b32 %3, 0, %3\n\t"
+      "s_pack_ll_b32_b16 %0, %3, %3"
+      : "=s"(r), "=&s"(a), "=&s"(c), "=&s"(t)
+      : "s"(v)
+      : "scc");
+  return r;
 }
 // v_bfi_b32 with an SGPR source for the selected bits
 __device__ __forceinline__ uint32_t vbfi_s(uint32_t mask, uint32_t a, uint32_t b) {
@@ -491,6 +511,44 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     // the x = 1 mask kept from the even step of a pair (step, MASK_PAIRS)
     constexpr bool MASK_PAIRS = VS && M == 2 && HSK == 2 && TSA_HM_TRACK;
     uint32_t m1_pair = 0u;
+    constexpr bool PRE = VS && TSA_PREINJ && !TSA_ABL_INJ && TSA_HM_TRACK;
+    // PRE: the injection of the step of phase PQN (the next one), into the
+    // registers that step reads: Ix (own), Ixy (the row above's record), Ixz and
+    // M (the z-shifted double buffers of its parity), and the per-row terms
+    auto vs_inject = [&](auto pqc) {
+      constexpr int PQN = decltype(pqc)::value;
+      constexpr int PHN = PQN & 1;
+      constexpr int ISN = M == 2 ? PHN : -1;  // skew 2, even P: the x = 1 register is the step's parity
+      int32_t ls, is, hs;
+      pos_split<M>(xpos0, ls, is, hs);
+      uint32_t m1;
+      if constexpr (MASK_PAIRS && (PQN & 1)) {
+        m1 = m1_pair;
+      } else {
+        asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(m1) : "v"(hmCur), "s"(1ull << ls));
+        if constexpr (MASK_PAIRS) m1_pair = m1;
+      }
+#pragma unroll
+      for (int i = 0; i < M; ++i) {
+        if (ISN >= 0 ? i == ISN : i == is) {
+          if constexpr (TSA_H_SALU) {
+            oIx[i] = vbfi_s(m1, Hr[PQN & 3], oIx[i]);
+            svIxy[i] = vbfi_s(m1, Hr[PQN & 3], svIxy[i]);
+            shIxz[PHN][i] = vbfi_s(m1, Hr[PQN & 3], shIxz[PHN][i]);
+            svM[PHN][i] = vbfi_s(m1, Hr[(PQN + 3) & 3], svM[PHN][i]);
+          } else {
+            oIx[i] = vbfi(m1, Hr[PQN & 3], oIx[i]);
+            svIxy[i] = vbfi(m1, Hr[PQN & 3], svIxy[i]);
+            shIxz[PHN][i] = vbfi(m1, Hr[PQN & 3], shIxz[PHN][i]);
+            svM[PHN][i] = vbfi(m1, Hr[(PQN + 3) & 3], svM[PHN][i]);
+          }
+          b[i] = vbfi(m1, binj, b[i]);
+          SBC[i] = vbfi(m1, SBCn[i], SBC[i]);
+          K[i] = vbfi(m1, Kn[i], K[i]);
+          DMB[i] = vbfi(m1, DMBn, DMB[i]);
+        }
+      }
+    };
     // One step; PH = t & 1 picks the register roles and the LDS record slots,
     // ROLE the wave's place in the lap (0: wave 0, reads the ring; 2: the last
     // wave, writes it; 1: the others), so the loop body has no role branches.
@@ -539,7 +597,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
       // ---- x == 1 at position k* = (t - w) mod P: its x-1 inputs are the x = 0
       // face (EN_i==1&&EN==0 gating, src/PE_1cyc.v:164-178,196-202,212-218), and
       // it starts row lap0*NW+w+1, whose B symbol it takes here.
-      if (!TSA_ABL_INJ && (TSA_HM_TRACK || xpos0 < KS)) {  // (tracked: hmCur is 0 past KS)
+      if (!PRE && !TSA_ABL_INJ && (TSA_HM_TRACK || xpos0 < KS)) {  // (tracked: hmCur is 0 past KS)
         int32_t ls, is, hs;
         pos_split<M>(xpos0, ls, is, hs);
 #if TSA_HM_TRACK
@@ -742,6 +800,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
           zshift<M>(svIyz, rz, sel, Hr[(PQ + 1) & 3]);
           zshift<M>(svM[PH], rw, sel, Hr[(PQ + 1) & 3]);
         }
+        if constexpr (PRE) vs_inject(std::integral_constant<int, (PQ + 1) & 3>{});  // the next step's x = 1
       } else {
         zshift<M>(shIxz[PH], oIxz, sel, pa.f_pair);  // z = 0 face for position 0
         zshift<M>(shIz, oIz, sel, pa.f_single);
@@ -819,6 +878,7 @@ __global__ __launch_bounds__(64 * NW) void pencil_kernel(const uint8_t *__restri
     // role | (w & 1) + 1 << 2 (M = 2, see ISC in step)
     constexpr int W0 = (M == 2 && TSA_IS_STATIC) ? 4 : 0, W1 = (M == 2 && TSA_IS_STATIC) ? 8 : 0;
     static_assert(NW % 2 == 0, "the last wave is odd");
+    if constexpr (PRE) vs_inject(std::integral_constant<int, 0>{});  // step 0's x = 1
     if (w == 0) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 0 + W0>{}));
     else if (w == NW - 1) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 2 + W1>{}));
     else if (W0 != 0 && (w & 1)) TSA_INLINE_IF_WIDE(run(std::integral_constant<int, 1 + W1>{}));
