@@ -66,14 +66,14 @@ constexpr int RING_EXTRA = 8;
 // V-space: the face values H(s) = lam q kept as wave-uniform integers and
 // encoded to f16 bits in SALU (f16x2_int), so they live in SGPRs: no VALU add
 // per step, and the bfi / perm that inject them read the SGPR directly
-#ifndef TSA_H_SALU
-#define TSA_H_SALU 1
+#ifndef TSA_H_SALU  // (measured slower: 1667 / 1645 vs 1697 / 1687 GCUPS, profiles/r5b_helix_ab.jsonl)
+#define TSA_H_SALU 0
 #endif
 // V-space: step s's x = 1 injection applied to the state registers at the end
 // of step s - 1 (before the step barrier), not to the inputs at the start of
 // step s, where it stood between the barrier and the cell
-#ifndef TSA_PREINJ
-#define TSA_PREINJ 1
+#ifndef TSA_PREINJ  // (measured neutral with TSA_H_SALU: 1646 / 1646 vs 1667 / 1645, r5b)
+#define TSA_PREINJ 0
 #endif
 // f16 bits of the integer v in both halves, exact for 0 <= v <= 2047 --
 // integer ops only, so a wave-uniform v stays in SALU (~8 instructions). The
