@@ -135,6 +135,32 @@ __device__ __forceinline__ void store16_sc1(void *gptr, uint4 v) {
   else
     asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(gptr), "v"(d) : "memory");
 }
+// the same store at sbase + voff + OFFB (SGPR base, 32-bit VGPR offset, immediate)
+template <bool SYS, int OFFB>
+__device__ __forceinline__ void store16_sc1_s(const uint8_t *sbase, uint32_t voff, uint4 v) {
+  static_assert(OFFB >= 0 && OFFB < 4096, "13-bit signed global offset");
+  const u32x4 d = {v.x, v.y, v.z, v.w};
+  if constexpr (SYS)
+    asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3 sc0 sc1\n\ts_nop 1" ::"v"(voff), "v"(d), "s"(sbase),
+                 "i"(OFFB)
+                 : "memory");
+  else
+    asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3 sc1\n\ts_nop 1" ::"v"(voff), "v"(d), "s"(sbase),
+                 "i"(OFFB)
+                 : "memory");
+}
+// the same store at gptr + OFFB (the instruction's immediate offset)
+template <bool SYS, int OFFB>
+__device__ __forceinline__ void store16_sc1_at(void *gptr, uint4 v) {
+  static_assert(OFFB >= 0 && OFFB < 4096, "13-bit signed global offset");
+  const u32x4 d = {v.x, v.y, v.z, v.w};
+  if constexpr (SYS)
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc0 sc1\n\ts_nop 1" ::"v"(gptr), "v"(d), "i"(OFFB)
+                 : "memory");
+  else
+    asm volatile("global_store_dwordx4 %0, %1, off offset:%2 sc1\n\ts_nop 1" ::"v"(gptr), "v"(d), "i"(OFFB)
+                 : "memory");
+}
 __device__ __forceinline__ uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
   return __builtin_amdgcn_perm(s0, s1, sel);
 }
@@ -509,6 +535,34 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 #ifndef TSA_LAP_Y2  // (measured: 64^3 / 256^3 / 512^3 0.5-1 % faster, profiles/r5a_lap_y2_ab.jsonl)
 #define TSA_LAP_Y2 1
 #endif
+// Four-step groups: a step's ring slots, z / y record addresses and next A
+// codes sit at constant offsets (instruction immediates) from bases set once
+// per group of four steps -- every ring length is a multiple of 4 and ZT of
+// LAP_ZL -- instead of being computed every step. The message forms' constant
+// y = 0 / z = 0 faces are prefilled into every slot of xr0 / zring (which the
+// loader then leaves alone), so the offsets never depend on yin / zin.
+#ifndef TSA_LAP_U4
+#define TSA_LAP_U4 1
+#endif
+// In a four-step group, the back-pressure checks batched: the consumers' ring
+// room once per group (for its last step; the rings hold >= 32 slots), the
+// successor wave's slot every other step for K = 4 (covering the next step:
+// it needs the successor past step t - 2 at the end of step t, which it
+// normally is, one step behind)
+#ifndef TSA_LAP_GCHK
+#define TSA_LAP_GCHK 1
+#endif
+// In a four-step group, every LDS base a step reads or writes (the input and
+// output record rings, the group's y / z ring slots, the two progress words)
+// held in a VGPR laundered once per lap / group, so each access is one ds
+// instruction with a constant offset; left alone the compiler keeps the
+// uniform part in SGPRs -- one per ring slot, spilled to VGPR lanes -- and
+// rebuilds every address with v_readlane / v_mov / v_add each step. The ring
+// records go out through the SGPR-base form of global_store (no 64-bit VGPR
+// address per store).
+#ifndef TSA_LAP_VBASE
+#define TSA_LAP_VBASE 1
+#endif
 __host__ __device__ constexpr int lap_waves_per_eu(int M, bool lit = false, bool chk = false) {
   return lit ? (M == 1 ? 4 : 3) : M == 1 ? (chk ? 4 : TSA_LAP_WPE1) : M == 2 ? (chk ? TSA_LAP_WPE2C : TSA_LAP_WPE2) : 2;
 }
@@ -588,6 +642,11 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
   static_assert(!VS || (F16 && !CHK && !LIT && !SYS), "V-space: the f16 single-device form");
   // the loader writes the step-varying y = 0 / z = 0 faces (LIT, VS)
   constexpr bool FACES = LIT || VS;
+  // four-step groups (TSA_LAP_U4) for M <= 2 (M = 4's checked form spills with
+  // them), their VGPR bases (TSA_LAP_VBASE) but for the M = 1 factored int16
+  // forms (at the 80-VGPR cap of two NW = 8 workgroups per CU they spill 8 bytes)
+  constexpr bool U4K = TSA_LAP_U4 && M <= 2;
+  constexpr bool VBK = TSA_LAP_VBASE && U4K && (F16 || LIT || M == 2);
   constexpr int SCOPE = SYS ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
   constexpr int RW = 2 * NW, ZT = 64 * M, LPD = lap_pd(M), K = lap_k(M), K0 = lap_k0(M);
   constexpr int PAIR = 64 * REC_BYTES, SLOT = M * PAIR;
@@ -753,6 +812,16 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
   if (tid < 2 * NW)
     ((uint4 *)zface)[tid] = (tid & 1) ? make_uint4(pa.f_pair, 0u, 0u, 0u)
                                                       : make_uint4(pa.f_single, 0u, pa.f_pair, 0u);
+  if constexpr (U4K && !FACES) {  // the same records in every ring slot (no loader writes)
+    if (!yin)
+      for (int j = tid; j < K0 * M * 64; j += 64 * (NW + 1))
+        ((uint4 *)xr0)[j] = make_uint4((pa.f_single & 0xFFFFu) | (pa.f_pair & 0xFFFF0000u), 0u,
+                                       pa.f_pair & 0xFFFFu, 0u);
+    if (!zin)
+      for (int j = tid; j < LAP_ZL * 2 * NW; j += 64 * (NW + 1))
+        ((uint4 *)zring)[j] = (j & 1) ? make_uint4(pa.f_pair, 0u, 0u, 0u)
+                                      : make_uint4(pa.f_single, 0u, pa.f_pair, 0u);
+  }
   pw[tid] = 0;  // blockDim = 64 (NW + 1): one word per thread
   // the wave-to-wave rings: step 0 reads slot K-1 before any write (its cells
   // are not real, but the checked kernel's monitor must not see stale LDS)
@@ -892,6 +961,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
     // sees those cells too, and must not see stale ring contents)
     auto put_z = [&](int32_t rz, const Fetch &f) {
       const bool real = rz < T_left;
+      if (U4K && !FACES && !zin) return;  // zring holds the prefilled z = 0 face
       if (lane < 2 * NW) {
         uint4 v = real ? make_uint4((uint32_t)f.z[0], (uint32_t)(f.z[0] >> 32), (uint32_t)f.z[1],
                                     (uint32_t)(f.z[1] >> 32))
@@ -939,18 +1009,21 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
       wait_word(pw + 64 * (NW - 1), seen_wl, s + ZA - LAP_ZL + 1);  // the last wave with zring's old record
       uint8_t *dst = xr0 + (s & (K0 - 1)) * SLOT + lane * REC_BYTES;
       const bool yreal = s + YOFF < T_above;
+      const bool ywrite = !(U4K && !FACES) || yin;  // else xr0 holds the prefilled y = 0 face
+      if (ywrite) {
 #pragma unroll
-      for (int i = 0; i < M; ++i) {
-        uint4 v = yreal ? make_uint4((uint32_t)f.y[2 * i], (uint32_t)(f.y[2 * i] >> 32),
-                                     (uint32_t)f.y[2 * i + 1], (uint32_t)(f.y[2 * i + 1] >> 32))
-                        : make_uint4(0u, 0u, 0u, 0u);
-        if constexpr (LIT) {
-          if (!yin) v = yface_lit(s, i);
+        for (int i = 0; i < M; ++i) {
+          uint4 v = yreal ? make_uint4((uint32_t)f.y[2 * i], (uint32_t)(f.y[2 * i] >> 32),
+                                       (uint32_t)f.y[2 * i + 1], (uint32_t)(f.y[2 * i + 1] >> 32))
+                          : make_uint4(0u, 0u, 0u, 0u);
+          if constexpr (LIT) {
+            if (!yin) v = yface_lit(s, i);
+          }
+          if constexpr (VS) {
+            if (!yin) v = yface_vs(s);
+          }
+          lds_write16(dst + i * PAIR, v);
         }
-        if constexpr (VS) {
-          if (!yin) v = yface_vs(s);
-        }
-        lds_write16(dst + i * PAIR, v);
       }
       put_z(rz, f);
       lds_publish(pw + 64 * NW, s + 1, lane);  // wave 0 may run step s
@@ -1071,14 +1144,53 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
     }
     // wave 0's y input: xr0 slot t % K0, or the face record (stride 0)
     // (LIT / VS: always the loader's, which writes the step-varying faces)
-    const uint8_t *const ysrc = ((yin || FACES) ? xr0 : yface) + lane * REC_BYTES;
-    const int32_t ystride = (yin || FACES) ? SLOT : 0;
-    // position 0's z input: zring slot (t + ZT) % ZL, or the face record
-    const uint8_t *const zsrc = ((zin || FACES) ? zring : zface) + w * LAP_ZREC_WAVE;
-    const int32_t zstride = (zin || FACES) ? ZREC : 0;
+    // (U4K: always xr0, which then holds the prefilled face)
+    const bool yring = U4K || yin || FACES, zring_in = U4K || zin || FACES;
+    const uint8_t *const ysrc = (yring ? xr0 : yface) + lane * REC_BYTES;
+    const int32_t ystride = yring ? SLOT : 0;
+    // position 0's z input: zring slot (t + ZT) % ZL = t % ZL, or the face record
+    static_assert(ZT % LAP_ZL == 0, "z slot of step t: t % LAP_ZL");
+    const uint8_t *const zsrc = (zring_in ? zring : zface) + w * LAP_ZREC_WAVE;
+    const int32_t zstride = zring_in ? ZREC : 0;
     uint32_t a_nx[M];
     load_a<M>(a_lane, a_nx);
     uint32_t a_pair = a_lane;  // TSA_LAP_LEAN: a_lane's entry of the step pair's first step
+    // U4K: the bases of the current group of four steps (t0 = t & ~3)
+    uint32_t a_grp = a_lane;
+    const uint8_t *y_grp = ysrc, *z_grp = zsrc;
+    uint8_t *zst_grp = nullptr, *yst_grp = nullptr;
+    // VBK: three VGPR bases (see the knob) -- v_rw: this lane's
+    // record in the ring read (slot 0; wave 0: the ring it writes), the ring
+    // written K slots above it; v_pwb: this lane's copy of the progress word
+    // of wave w - 1 (wave 0: its own), the others at constant offsets above
+    // it (every lane holds a copy, so a per-lane address reads the same
+    // value); vlane: the SGPR-base stores' offset (the z record, stored by lane
+    // 63, from a base 63 records lower)
+    lds_u8 *v_rw = to_lds(xr + (w > 0 ? (w - 1) * K * SLOT : 0) + lane * REC_BYTES);
+    lds_u8 *v_pwb = to_lds((uint8_t *)(pw + 64 * (w > 0 ? w - 1 : 0) + lane));
+    // byte offsets from v_pwb: the input word (wave 0: the loader's), the own, the successor's
+    auto pw_in = [](auto role) { return decltype(role)::value == 0 ? 4 * 64 * NW : 0; };
+    auto pw_own = [](auto role) { return decltype(role)::value == 0 ? 0 : 4 * 64; };
+    constexpr int WR_OFF = K * SLOT;  // v_rw + WR_OFF: the ring written (waves 1 ..)
+    const lds_u8 *vy_grp = to_lds((uint8_t *)ysrc), *vz_grp = to_lds((uint8_t *)zsrc);
+    const uint8_t *zst_s = zf_mine, *yst_s = yf_mine;  // SGPR bases of the group's ring records
+    uint32_t vlane = (uint32_t)lane * REC_BYTES;
+    if constexpr (VBK) asm volatile("" : "+v"(v_rw), "+v"(v_pwb), "+v"(vlane));
+    auto set_group = [&](int32_t t0) {
+      a_grp = a_lane + 4u * (uint32_t)t0;
+      y_grp = ysrc + (t0 & (K0 - 1)) * SLOT;
+      z_grp = zsrc + (t0 & (LAP_ZL - 1)) * ZREC;
+      zst_grp = zf_mine + (int64_t)(t0 & (ZRm - 1)) * ZREC + w * LAP_ZREC_WAVE;
+      yst_grp = yf_mine + (int64_t)(t0 & (YRm - 1)) * SLOT + lane * REC_BYTES;
+      if constexpr (VBK) {
+        vy_grp = to_lds((uint8_t *)y_grp);
+        vz_grp = to_lds((uint8_t *)z_grp);
+        asm volatile("" : "+v"(vy_grp), "+v"(vz_grp));
+        zst_s = (const uint8_t *)sgpr64((uint64_t)(uintptr_t)(zf_mine + (int64_t)(t0 & (ZRm - 1)) * ZREC +
+                                                              w * LAP_ZREC_WAVE - 63 * REC_BYTES));
+        yst_s = (const uint8_t *)sgpr64((uint64_t)(uintptr_t)(yf_mine + (int64_t)(t0 & (YRm - 1)) * SLOT));
+      }
+    };
     // producer side: my consumers' progress (y: the lap below, via the last
     // wave; z: the tile to the right, every wave), LDS-DMA'd by the loader
     int32_t seen_in = 0, seen_out = 0, seen_y = 0, seen_z = 0;
@@ -1112,16 +1224,31 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
       }
     };
     const int64_t cons_y = yout ? lid + GZ : -1, cons_z = zout ? lid + 1 : -1;
+    // Room in my z ring for record tt: the consumer's loader checks record
+    // s + ZT + ZA at its step s, so a published progress p covers records up
+    // to p - 1 + ZT + ZA -- and its prologue reads ZT - 2 .. ZT + ZA - 1
+    // before it publishes anything, so overwriting one of those (or later)
+    // needs p >= 1 even where that formula gives <= 0: a consumer that starts
+    // late (its physical workgroup still on a lap of the previous round) would
+    // otherwise find its prologue records overwritten and wait forever
+    auto z_need = [&](int32_t tt) -> int32_t {
+      const int32_t r = tt - ZRm;  // the record slot tt & (ZRm - 1) holds before
+      return r >= ZT - 2 ? max(1, r - ZT - ZA + 1) : 0;
+    };
 
     // ROLE: 0 = wave 0, 1 = middle waves, 2 = the last wave (NW >= 2)
-    auto step = [&](auto ph, auto role, int32_t t, auto fin_step) {
+    // QS: t & 3 in a four-step group (addresses at constant offsets from the
+    // group's bases), -1: addresses from t
+    auto step = [&](auto ph, auto role, int32_t t, auto fin_step, auto qs) {
       constexpr int PH = decltype(ph)::value;
       constexpr int ROLE = decltype(role)::value;
       constexpr bool FIN = decltype(fin_step)::value;
+      constexpr int QS = decltype(qs)::value;
       uint32_t a[M];
 #pragma unroll
       for (int i = 0; i < M; ++i) a[i] = a_nx[i];
-      if constexpr (TSA_LAP_LEAN) load_a_off<M>(a_pair, PH + 1, a_nx);  // entry t + 1 of a_lane's table
+      if constexpr (QS >= 0) load_a_off<M>(a_grp, QS + 1, a_nx);
+      else if constexpr (TSA_LAP_LEAN) load_a_off<M>(a_pair, PH + 1, a_nx);  // entry t + 1 of a_lane's table
       else load_a<M>(a_lane + 4u * (uint32_t)(t + 1), a_nx);
       // ---- input reads, issued first: the producer's progress word (unless the
       // cached value covers step t), then its record. LDS executes a wave's DS
@@ -1135,42 +1262,53 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
       const bool waits = ROLE != 0 || yin || zin || FACES;
       const bool poll = TSA_LAP_LEAN ? waits : (waits && seen_in < need);
       int32_t fl_v = 0;
-      if (poll)
-        fl_v = *(volatile const __attribute__((address_space(3))) int32_t *)(
-            const __attribute__((address_space(3))) void *)pword;
+      constexpr bool VB = QS >= 0 && VBK;  // this step's accesses off the VGPR bases
+      if (poll) {
+        if constexpr (VB)
+          fl_v = *(volatile const __attribute__((address_space(3))) int32_t *)(v_pwb + pw_in(role));
+        else
+          fl_v = *(volatile const __attribute__((address_space(3))) int32_t *)(
+              const __attribute__((address_space(3))) void *)pword;
+      }
       asm volatile("" ::: "memory");
-      const uint8_t *src = ROLE == 0 ? ysrc + (t & (K0 - 1)) * ystride
+      const uint8_t *src = QS >= 0 ? (ROLE == 0 ? y_grp + QS * SLOT
+                                                : xr + ((w - 1) * K + ((QS + K - 1) & (K - 1))) * SLOT + lane * REC_BYTES)
+                         : ROLE == 0 ? ysrc + (t & (K0 - 1)) * ystride
                                      : xr + ((w - 1) * K + ((t - 1) & (K - 1))) * SLOT + lane * REC_BYTES;
+      const lds_u8 *srcl = VB ? (ROLE == 0 ? vy_grp + (VB ? QS : 0) * SLOT
+                                           : v_rw + (((VB ? QS : 0) + K - 1) & (K - 1)) * SLOT)
+                              : to_lds((uint8_t *)src);
       uint4 rv[M];
       auto read_rec = [&]() {
 #pragma unroll
         for (int i = 0; i < M; ++i) {
           if constexpr (ROLE == 0 && TSA_LAP_Y2) {  // {payload, tag, payload, tag}: the payloads only
             const __attribute__((address_space(3))) uint32_t *p =
-                (const __attribute__((address_space(3))) uint32_t *)(const __attribute__((address_space(3))) void *)(
-                    src + i * PAIR);
+                (const __attribute__((address_space(3))) uint32_t *)(srcl + i * PAIR);
             rv[i] = make_uint4(p[0], 0u, p[2], 0u);
           } else {
-            rv[i] = lds_read16(src + i * PAIR);
+            rv[i] = lds_read16_at(srcl, i * PAIR);
           }
         }
       };
       read_rec();
       // the successor's progress, read now and consulted before the record store
+      // (TSA_LAP_GCHK groups, K = 4: on even steps only, covering the next step too)
+      constexpr bool SUCC_HERE = !(QS >= 0 && TSA_LAP_GCHK && K == 4) || (QS & 1) == 0;
       int32_t succ_v = 0;
-      if constexpr (ROLE != 2)
+      if constexpr (ROLE != 2 && SUCC_HERE && VB)
+        succ_v = *(volatile const __attribute__((address_space(3))) int32_t *)(v_pwb + pw_own(role) + 4 * 64);
+      else if constexpr (ROLE != 2 && SUCC_HERE)
         succ_v = *(volatile const __attribute__((address_space(3))) int32_t *)(
             const __attribute__((address_space(3))) void *)(pw + 64 * (w + 1));
       // position 0's z-1 neighbour for the next step: the z = 0 face, or the
       // left tile's record t + ZT (checked by the loader: see ZA)
       // (four 4-byte reads, merged into two ds_read2_b32: reading the tags too
       // hands the compiler dead registers it reuses, forcing lgkmcnt(0) waits)
-      const uint8_t *zr = zsrc + ((t + ZT) & (LAP_ZL - 1)) * zstride;
-      auto lds32 = [](const uint8_t *p) {
-        return *(const __attribute__((address_space(3))) uint32_t *)(
-            const __attribute__((address_space(3))) void *)p;
-      };
-      const uint32_t fIz = lds32(zr), fIxz = lds32(zr + 8), fIyz = lds32(zr + 16), fM = lds32(zr + 24);
+      const uint8_t *zr = QS >= 0 ? z_grp + QS * ZREC : zsrc + ((t + ZT) & (LAP_ZL - 1)) * zstride;
+      const lds_u8 *zrl = VB ? vz_grp + (VB ? QS : 0) * ZREC : to_lds((uint8_t *)zr);
+      auto lds32 = [](const lds_u8 *p) { return *(const __attribute__((address_space(3))) uint32_t *)p; };
+      const uint32_t fIz = lds32(zrl), fIxz = lds32(zrl + 8), fIyz = lds32(zrl + 16), fM = lds32(zrl + 24);
       uint32_t inIx[M], inIz[M], inIxy[M], inIyz[M], inIxz[M], inM[M];
 #pragma unroll
       for (int i = 0; i < M; ++i) {
@@ -1310,28 +1448,42 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
       }
       // ---- records: to the wave below (LDS), or (last wave) the y ring
       if constexpr (ROLE != 2) {
-        seen_out = max(seen_out, (int32_t)__builtin_amdgcn_readfirstlane(succ_v));
-        wait_word(pw + 64 * (w + 1), seen_out, t - K + 2);  // wave w+1 read slot t % K's old record
-        uint8_t *dst = xr + (w * K + (t & (K - 1))) * SLOT + lane * REC_BYTES;
+        if constexpr (SUCC_HERE) {
+          constexpr int AHEAD = (QS >= 0 && TSA_LAP_GCHK && K == 4) ? 1 : 0;
+          seen_out = max(seen_out, (int32_t)__builtin_amdgcn_readfirstlane(succ_v));
+          wait_word(pw + 64 * (w + 1), seen_out, t + AHEAD - K + 2);  // wave w+1 read slot t % K's old record
+        }
+        uint8_t *dst = xr + (w * K + ((QS >= 0 ? QS : t) & (K - 1))) * SLOT + lane * REC_BYTES;
 #pragma unroll
-        for (int i = 0; i < M; ++i)
-          lds_write16(dst + i * PAIR, make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]));
+        for (int i = 0; i < M; ++i) {
+          const uint4 v = make_uint4(oIy[i], oIxy[i], oIyz[i], oBest[i]);
+          if constexpr (VB) lds_write16_at(v_rw, (ROLE == 0 ? 0 : WR_OFF) + ((VB ? QS : 0) & (K - 1)) * SLOT + i * PAIR, v);
+          else lds_write16(dst + i * PAIR, v);
+        }
       } else {
         if (yout) {
 #if defined(TSA_DIAG)
           lag_y = max(lag_y, t - prog_decode(lds_word(bpw)));
 #endif
-          wait_consumer(cons_y, seen_y, bpw, t - YRm - YOFF + 1);
+          // (TSA_LAP_GCHK groups: once per group, for its last step)
+          if (!(QS >= 0 && TSA_LAP_GCHK)) wait_consumer(cons_y, seen_y, bpw, t - YRm - YOFF + 1);
+          else if (QS == 0) wait_consumer(cons_y, seen_y, bpw, t + 3 - YRm - YOFF + 1);
           const uint32_t tg = lap_tag(epoch, t);
-#pragma unroll
-          for (int i = 0; i < M; ++i)
-            store16_sc1<SYS>(yf_mine + ((int64_t)(t & (YRm - 1)) * M + i) * PAIR + lane * REC_BYTES,
-                        make_uint4(perm(oIxy[i], oIy[i], 0x07060302u), tg,
-                                   perm(oBest[i], oIyz[i], 0x07060302u), tg));
+          static_for<0, M>([&](auto ii) {
+            constexpr int i = decltype(ii)::value;
+            const uint4 v = make_uint4(perm(oIxy[i], oIy[i], 0x07060302u), tg,
+                                       perm(oBest[i], oIyz[i], 0x07060302u), tg);
+            constexpr int OFFB = (QS * M + i) * PAIR;
+            if constexpr (VB && OFFB < 4096) store16_sc1_s<SYS, (VB ? OFFB : 0)>(yst_s, vlane, v);
+            else if constexpr (QS >= 0 && OFFB < 4096) store16_sc1_at<SYS, OFFB>(yst_grp, v);
+            else if constexpr (QS >= 0) store16_sc1<SYS>(yst_grp + OFFB, v);
+            else store16_sc1<SYS>(yf_mine + ((int64_t)(t & (YRm - 1)) * M + i) * PAIR + lane * REC_BYTES, v);
+          });
         }
         // my producers' back-pressure: the loader has checked at least
         // t - NW + 2 steps (wave 0 ran t - NW + 1 before this wave's step t)
-        if ((yin || zin) && (t & (LAP_PUB - 1)) == 0 && lane == 0)
+        const bool pub_step = (QS >= 0 && LAP_PUB == 4) ? QS == 0 : (t & (LAP_PUB - 1)) == 0;
+        if ((yin || zin) && pub_step && lane == 0)
         {
           const int32_t pv_ = (int32_t)((ep19 << 13) | (uint32_t)max(t - NW + 2, 0));
           __hip_atomic_store(prog + lid * LAP_PROG_STRIDE, pv_, __ATOMIC_RELAXED, SCOPE);
@@ -1345,15 +1497,30 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
 #if defined(TSA_DIAG)
         lag_z = max(lag_z, t - prog_decode(lds_word(bpw + 1)));
 #endif
-        wait_consumer(cons_z, seen_z, bpw + 1, t - ZRm - ZT - ZA + 1);
+        if (!(QS >= 0 && TSA_LAP_GCHK)) wait_consumer(cons_z, seen_z, bpw + 1, z_need(t));
+        else if (QS == 0) wait_consumer(cons_z, seen_z, bpw + 1, z_need(t + 3));
         if (lane == 63) {
           const uint32_t tg = lap_tag(epoch, t);
-          uint8_t *zdst = zf_mine + (int64_t)(t & (ZRm - 1)) * ZREC + w * LAP_ZREC_WAVE;
-          store16_sc1<SYS>(zdst, make_uint4(oIz[M - 1], tg, oIxz[M - 1], tg));
-          store16_sc1<SYS>(zdst + 16, make_uint4(Ryz[M - 1], tg, Rb[M - 1], tg));
+          if constexpr (VB) {
+            store16_sc1_s<SYS, (VB ? QS : 0) * ZREC>(zst_s, vlane, make_uint4(oIz[M - 1], tg, oIxz[M - 1], tg));
+            store16_sc1_s<SYS, (VB ? QS : 0) * ZREC + 16>(zst_s, vlane, make_uint4(Ryz[M - 1], tg, Rb[M - 1], tg));
+          } else if constexpr (QS >= 0) {
+            store16_sc1_at<SYS, (QS >= 0 ? QS : 0) * ZREC>(zst_grp, make_uint4(oIz[M - 1], tg, oIxz[M - 1], tg));
+            store16_sc1_at<SYS, (QS >= 0 ? QS : 0) * ZREC + 16>(zst_grp, make_uint4(Ryz[M - 1], tg, Rb[M - 1], tg));
+          } else {
+            uint8_t *zdst = zf_mine + (int64_t)(t & (ZRm - 1)) * ZREC + w * LAP_ZREC_WAVE;
+            store16_sc1<SYS>(zdst, make_uint4(oIz[M - 1], tg, oIxz[M - 1], tg));
+            store16_sc1<SYS>(zdst + 16, make_uint4(Ryz[M - 1], tg, Rb[M - 1], tg));
+          }
         }
       }
-      lds_publish(pw + 64 * w, t + 1, lane);
+      if constexpr (VB) {  // lds_publish through the base
+        asm volatile("" ::: "memory");
+        *(volatile __attribute__((address_space(3))) int32_t *)(v_pwb + pw_own(role)) = t + 1;
+        asm volatile("" ::: "memory");
+      } else {
+        lds_publish(pw + 64 * w, t + 1, lane);
+      }
 #if defined(TSA_DIAG)
       const uint64_t pt3 = __builtin_amdgcn_s_memtime();
       prof[0] += pt1 - pt0;
@@ -1384,18 +1551,33 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
       constexpr std::integral_constant<int, 1> P1{};
       constexpr std::false_type mid{};
       constexpr std::true_type last{};
+      constexpr std::integral_constant<int, -1> QD{};
+      if constexpr (U4K) {
+        constexpr std::integral_constant<int, 0> Q0{};
+        constexpr std::integral_constant<int, 1> Q1{};
+        constexpr std::integral_constant<int, 2> Q2{};
+        constexpr std::integral_constant<int, 3> Q3{};
+#pragma unroll 1
+        for (; t + 3 < T1; t += 4) {
+          set_group(t);
+          LAP_INLINE(step(P0, role, t, mid, Q0));
+          LAP_INLINE(step(P1, role, t + 1, mid, Q1));
+          LAP_INLINE(step(P0, role, t + 2, mid, Q2));
+          LAP_INLINE(step(P1, role, t + 3, mid, Q3));
+        }
+      }
 #pragma unroll 1
       for (; t + 1 < T1; t += 2) {
         a_pair = a_lane + 4u * (uint32_t)t;
-        LAP_INLINE(step(P0, role, t, mid));
-        LAP_INLINE(step(P1, role, t + 1, mid));
+        LAP_INLINE(step(P0, role, t, mid, QD));
+        LAP_INLINE(step(P1, role, t + 1, mid, QD));
       }
       a_pair = a_lane + 4u * (uint32_t)t;
       if (t < T1) {
-        LAP_INLINE(step(P0, role, t, mid));
-        LAP_INLINE(step(P1, role, t + 1, last));
+        LAP_INLINE(step(P0, role, t, mid, QD));
+        LAP_INLINE(step(P1, role, t + 1, last, QD));
       } else {
-        LAP_INLINE(step(P0, role, t, last));
+        LAP_INLINE(step(P0, role, t, last, QD));
       }
     };
     static_assert(NW >= 2, "wave 0 and the last wave are distinct roles");

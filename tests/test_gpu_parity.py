@@ -409,6 +409,31 @@ def test_lap_looped_rounds_several_per_cu(gpu, orc, monkeypatch):
     assert np.array_equal(d_sc.cpu().numpy(), ref), plan
 
 
+def test_lap_late_consumer_keeps_its_prologue_records(gpu, orc, monkeypatch):
+    """One workgroup per CU, three looped rounds, slim z rings (600^3, int16,
+    M = 1, NW = 8): a round-2 z consumer starts only when its physical
+    workgroup finishes a round-1 lap, while its producer, resident earlier,
+    runs ahead. The producer must not overwrite the records the consumer's
+    loader prologue reads (ZT - 2 .. ZT + ZA - 1) before the consumer has
+    published any progress -- the z back-pressure once counted them consumed
+    at progress 0, and the four-step groups made the producer fast enough to
+    overwrite them: every such launch timed out (TSA_SCORE_INVALID)."""
+    monkeypatch.setenv("TSA_PENCIL_MODE", "lap")
+    monkeypatch.setenv("TSA_LAP_M", "1")
+    monkeypatch.setenv("TSA_LAP_NW", "8")
+    monkeypatch.setenv("TSA_PENCIL_ARITH", "i16")
+    L = 600
+    rng = np.random.default_rng(600)
+    a, b, c = (rng.integers(0, 4, L).astype(np.uint8) for _ in range(3))
+    p = gpu.TsaParams.default(score_bits=16)
+    plan = gpu.describe_plan(1, L, L, L, p, "pencil", sync=False)
+    kv = dict(f.split("=") for f in plan.split() if "=" in f)
+    assert " i16 " in plan and int(kv["waves"]) >= 2 and int(kv["wpc"]) == 1, plan
+    ref = orc.score(a, b, c, orc.default_params(score_bits=16))
+    for _ in range(3):
+        assert _score_async(gpu, [(a, b, c)], p, "pencil", L)[0] == ref, plan
+
+
 def test_pencil_ragged_batch(gpu, orc):
     rng = np.random.default_rng(77)
     triples = []
