@@ -563,6 +563,29 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 #ifndef TSA_LAP_VBASE
 #define TSA_LAP_VBASE 1
 #endif
+// The loader fetches each ring record (two {payload, tag} granules) with one
+// 16-byte load instead of two 8-byte ones: 2M + 2 load instructions per step
+// become M + 1 (plus the progress words). 0: two 8-byte atomic loads; 1: a
+// volatile 16-byte load (measured 1.8x slower: the memory legalizer follows
+// each volatile load with vmcnt(0), serialising the fetch window,
+// profiles/r5f_lap_loader_ab.jsonl); 2: a raw buffer load with sc1 (counted by
+// the compiler like the atomics); -1 (default): 2 for the factored M = 1 forms,
+// 0 for the rest (profiles/r5i_lap_loader_ab.jsonl: with the progress words
+// every 4 steps, 64^3 / 256^3 / 512^3 5-6 % faster; the M = 2 checked and the
+// literal M = 1 forms neutral to 1 % slower)
+#ifndef TSA_LAP_L16
+#define TSA_LAP_L16 -1
+#endif
+// The consumers' progress words (the producers' back-pressure input, relayed
+// through LDS) fetched every TSA_LAP_PROGP steps instead of every step: fewer
+// loads in the loader's window (the consumers publish every LAP_PUB = 4 steps
+// anyway; a staler relay only waits more, never less). The loader loop then
+// runs in periods of max(LPD, PROGP) steps with a static phase. -1 (default):
+// 4 for the factored M = 1 forms, 2 for the rest (profiles/r5h_lap_prog_ab.jsonl,
+// r5i_lap_loader_ab.jsonl).
+#ifndef TSA_LAP_PROGP
+#define TSA_LAP_PROGP -1
+#endif
 __host__ __device__ constexpr int lap_waves_per_eu(int M, bool lit = false, bool chk = false) {
   return lit ? (M == 1 ? 4 : 3) : M == 1 ? (chk ? 4 : TSA_LAP_WPE1) : M == 2 ? (chk ? TSA_LAP_WPE2C : TSA_LAP_WPE2) : 2;
 }
@@ -647,6 +670,10 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
   // forms (at the 80-VGPR cap of two NW = 8 workgroups per CU they spill 8 bytes)
   constexpr bool U4K = TSA_LAP_U4 && M <= 2;
   constexpr bool VBK = TSA_LAP_VBASE && U4K && (F16 || LIT || M == 2);
+  // the loader's record loads and progress-word period (TSA_LAP_L16 / _PROGP)
+  constexpr bool FM1 = M == 1 && !LIT;
+  constexpr int L16K = TSA_LAP_L16 >= 0 ? TSA_LAP_L16 : FM1 ? 2 : 0;
+  constexpr int PROGPK = TSA_LAP_PROGP >= 0 ? TSA_LAP_PROGP : FM1 ? 4 : 2;
   constexpr int SCOPE = SYS ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
   constexpr int RW = 2 * NW, ZT = 64 * M, LPD = lap_pd(M), K = lap_k(M), K0 = lap_k0(M);
   constexpr int PAIR = 64 * REC_BYTES, SLOT = M * PAIR;
@@ -837,6 +864,25 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
     // written to LDS (xr0 / zring) and published.
     uint32_t stalls = 0;
     typedef unsigned long long u64;
+    // TSA_LAP_L16: a record's two granules by one 16-byte load (volatile:
+    // sc0 sc1, L1 bypassed, L2-served; each naturally aligned 8-byte {payload,
+    // tag} granule of it is untorn, so the per-granule tag check stands)
+    typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+    auto gl16 = [&](const uint8_t *p) -> u64x2 {
+      return *(volatile const __attribute__((address_space(1))) u64x2 *)(
+          const __attribute__((address_space(1))) void *)p;
+    };
+    // TSA_LAP_L16 = 2: the same 16 bytes by a raw buffer load with sc1 (a
+    // compiler-counted load, no vmcnt(0) behind it), off a per-lap resource
+    // of the ring's base
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)yf_prev, (short)0, 0x7FFFFFFF, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rzr = __builtin_amdgcn_make_buffer_rsrc((void *)zf_prev, (short)0, 0x7FFFFFFF, 0x00020000);
+    auto bl16 = [&](__amdgpu_buffer_rsrc_t r, uint32_t off) -> u64x2 {
+      if constexpr (SYS)  // 17: sc0 sc1 (system scope, as the 8-byte loads of the split)
+        return __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 17));
+      else  // 16: sc1
+        return __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+    };
     auto gl8 = [&](const uint8_t *p) -> u64 {
       return __hip_atomic_load((const u64 *)p, __ATOMIC_RELAXED, SCOPE);
     };
@@ -850,20 +896,42 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
 #pragma unroll
       for (int i = 0; i < M; ++i) {
         const uint8_t *g = yf_prev + ((int64_t)(r & (YRp - 1)) * M + i) * PAIR + lane * REC_BYTES;
-        f.y[2 * i] = gl8(g);
-        f.y[2 * i + 1] = gl8(g + 8);
+        if constexpr (L16K == 2) {
+          const u64x2 v = bl16(ry, (uint32_t)(((int64_t)(r & (YRp - 1)) * M + i) * PAIR + lane * REC_BYTES));
+          f.y[2 * i] = v[0];
+          f.y[2 * i + 1] = v[1];
+        } else if constexpr (L16K == 1) {
+          const u64x2 v = gl16(g);
+          f.y[2 * i] = v[0];
+          f.y[2 * i + 1] = v[1];
+        } else {
+          f.y[2 * i] = gl8(g);
+          f.y[2 * i + 1] = gl8(g + 8);
+        }
       }
     };
     auto fetch_z = [&](int32_t rz, Fetch &f) {  // z record rz (lanes 0 .. 2NW-1)
       const uint8_t *g = zf_prev + (int64_t)(rz & (ZRp - 1)) * ZREC + (lane & (2 * NW - 1)) * 16;
-      f.z[0] = gl8(g);
-      f.z[1] = gl8(g + 8);
+      if constexpr (L16K == 2) {
+        const u64x2 v = bl16(rzr, (uint32_t)((int64_t)(rz & (ZRp - 1)) * ZREC + (lane & (2 * NW - 1)) * 16));
+        f.z[0] = v[0];
+        f.z[1] = v[1];
+      } else if constexpr (L16K == 1) {
+        const u64x2 v = gl16(g);
+        f.z[0] = v[0];
+        f.z[1] = v[1];
+      } else {
+        f.z[0] = gl8(g);
+        f.z[1] = gl8(g + 8);
+      }
     };
-    auto fetch = [&](int32_t s, Fetch &f) {
+    auto fetch = [&](int32_t s, Fetch &f, bool progw = true) {
       fetch_y(s, f);
       fetch_z(s + ZT + ZA, f);
-      f.py = __hip_atomic_load(prog + cons_y * LAP_PROG_STRIDE, __ATOMIC_RELAXED, SCOPE);
-      f.pz = __hip_atomic_load(prog + cons_z * LAP_PROG_STRIDE, __ATOMIC_RELAXED, SCOPE);
+      if (progw) {
+        f.py = __hip_atomic_load(prog + cons_y * LAP_PROG_STRIDE, __ATOMIC_RELAXED, SCOPE);
+        f.pz = __hip_atomic_load(prog + cons_z * LAP_PROG_STRIDE, __ATOMIC_RELAXED, SCOPE);
+      }
     };
     // LIT: the y = 0 (lap 0) and z = 0 (tile 0) faces, written into the rings
     // wave 0 and position 0 read: zero cells pushing with the receivers'
@@ -991,17 +1059,23 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
     }
     __syncthreads();  // (matches the compute waves' prologue barrier)
     Fetch fq[LPD];
+    // the loop period LU (a multiple of LPD): the progress words ride with the
+    // fetch processed at phase 0 of a period, issued LPD steps earlier
+    constexpr bool PTHIN = PROGPK > 1;
+    constexpr int LU = (PROGPK > LPD && PROGPK % LPD == 0) ? PROGPK : LPD;
 #pragma unroll
-    for (int j = 0; j < LPD; ++j) fetch(j, fq[j]);
+    for (int j = 0; j < LPD; ++j) fetch(j, fq[j], !PTHIN || j == 0);
     // one step: check the fetch of step s (registers fq[j]), store it to LDS,
     // publish, refill fq[j] with step s + LPD
-    auto lstep = [&](auto jj, int32_t s) {
-      constexpr int j = decltype(jj)::value;
+    auto lstep = [&](auto ph, int32_t s) {
+      constexpr int PHL = decltype(ph)::value;  // phase in the loop period
+      constexpr int j = PHL % LPD;
       Fetch &f = fq[j];
       if (yin && s + YOFF < T_above && !y_ok(s, f)) settle_y(s, f);
       const int32_t rz = s + ZT + ZA;
       if (zin && rz < T_left && !z_ok(rz, f)) settle_z(rz, f);
-      if (lane == 0) {  // my consumers' progress, for the producing waves' back-pressure
+      constexpr bool PROGW = !PTHIN || PHL == 0;  // this fetch carries the progress words
+      if (PROGW && lane == 0) {  // my consumers' progress, for the producing waves' back-pressure
         bpw[0] = f.py;
         bpw[1] = f.pz;
       }
@@ -1027,14 +1101,14 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
       }
       put_z(rz, f);
       lds_publish(pw + 64 * NW, s + 1, lane);  // wave 0 may run step s
-      fetch(s + LPD, f);
+      fetch(s + LPD, f, !PTHIN || (PHL + LPD) % LU == 0);
     };
     int32_t s = 0;
 #pragma unroll 1
-    for (; s + LPD <= T; s += LPD)
-      static_for<0, LPD>([&](auto jj) { LAP_INLINE(lstep(jj, s + decltype(jj)::value)); });
-    static_for<0, LPD>([&](auto jj) {
-      if (s + decltype(jj)::value < T) LAP_INLINE(lstep(jj, s + decltype(jj)::value));
+    for (; s + LU <= T; s += LU)
+      static_for<0, LU>([&](auto ph) { LAP_INLINE(lstep(ph, s + decltype(ph)::value)); });
+    static_for<0, LU>([&](auto ph) {
+      if (s + decltype(ph)::value < T) LAP_INLINE(lstep(ph, s + decltype(ph)::value));
     });
     if (lane == 0) w_stall[0] = (int32_t)stalls;
   } else {
