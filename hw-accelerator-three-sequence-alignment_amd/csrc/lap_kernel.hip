@@ -569,10 +569,11 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 // volatile 16-byte load (measured 1.8x slower: the memory legalizer follows
 // each volatile load with vmcnt(0), serialising the fetch window,
 // profiles/r5f_lap_loader_ab.jsonl); 2: a raw buffer load with sc1 (counted by
-// the compiler like the atomics); -1 (default): 2 for the factored M = 1 forms,
-// 0 for the rest (profiles/r5i_lap_loader_ab.jsonl: with the progress words
-// every 4 steps, 64^3 / 256^3 / 512^3 5-6 % faster; the M = 2 checked and the
-// literal M = 1 forms neutral to 1 % slower)
+// the compiler like the atomics); -1 (default): 2 for the M = 1 forms, 0 for
+// the rest (with the progress words every 4 steps: factored 64^3 / 256^3 /
+// 512^3 5-6 % faster, profiles/r5i_lap_loader_ab.jsonl; literal 512^3 / 1024^3
+// 5 / 4 % faster, r5j_lap_loader_lit_ab.jsonl; the M = 2 checked 1024^3
+// neutral)
 #ifndef TSA_LAP_L16
 #define TSA_LAP_L16 -1
 #endif
@@ -581,10 +582,16 @@ __device__ __forceinline__ uint32_t lit_face_m(const LitArgs &cv, uint32_t an, u
 // loads in the loader's window (the consumers publish every LAP_PUB = 4 steps
 // anyway; a staler relay only waits more, never less). The loader loop then
 // runs in periods of max(LPD, PROGP) steps with a static phase. -1 (default):
-// 4 for the factored M = 1 forms, 2 for the rest (profiles/r5h_lap_prog_ab.jsonl,
-// r5i_lap_loader_ab.jsonl).
+// 4 for the M = 1 forms, 2 for the rest (profiles/r5h_lap_prog_ab.jsonl,
+// r5i_lap_loader_ab.jsonl, r5j_lap_loader_lit_ab.jsonl).
 #ifndef TSA_LAP_PROGP
 #define TSA_LAP_PROGP -1
+#endif
+// With the buffer loads (TSA_LAP_L16 = 2): the fetches a lap-0 / tile-0 loader
+// does not need (its y / z inputs are faces) out of range, so no memory access
+// (measured neutral: 64^3 - 512^3 within 0.5 %, profiles/r5j_lap_noface_ab.jsonl)
+#ifndef TSA_LAP_NOFACE_FETCH
+#define TSA_LAP_NOFACE_FETCH 1
 #endif
 __host__ __device__ constexpr int lap_waves_per_eu(int M, bool lit = false, bool chk = false) {
   return lit ? (M == 1 ? 4 : 3) : M == 1 ? (chk ? 4 : TSA_LAP_WPE1) : M == 2 ? (chk ? TSA_LAP_WPE2C : TSA_LAP_WPE2) : 2;
@@ -671,7 +678,7 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
   constexpr bool U4K = TSA_LAP_U4 && M <= 2;
   constexpr bool VBK = TSA_LAP_VBASE && U4K && (F16 || LIT || M == 2);
   // the loader's record loads and progress-word period (TSA_LAP_L16 / _PROGP)
-  constexpr bool FM1 = M == 1 && !LIT;
+  constexpr bool FM1 = M == 1;
   constexpr int L16K = TSA_LAP_L16 >= 0 ? TSA_LAP_L16 : FM1 ? 2 : 0;
   constexpr int PROGPK = TSA_LAP_PROGP >= 0 ? TSA_LAP_PROGP : FM1 ? 4 : 2;
   constexpr int SCOPE = SYS ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
@@ -875,8 +882,14 @@ __global__ __launch_bounds__(64 * (NW + 1), lap_waves_per_eu(M, LIT, CHK)) void 
     // TSA_LAP_L16 = 2: the same 16 bytes by a raw buffer load with sc1 (a
     // compiler-counted load, no vmcnt(0) behind it), off a per-lap resource
     // of the ring's base
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)yf_prev, (short)0, 0x7FFFFFFF, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rzr = __builtin_amdgcn_make_buffer_rsrc((void *)zf_prev, (short)0, 0x7FFFFFFF, 0x00020000);
+    // (TSA_LAP_NOFACE_FETCH: a lap-0 / tile-0 loader, whose y / z fetches feed
+    // nothing, gets a zero-length resource -- its loads stay in the window, so
+    // the compiler's vmcnt counting stays static, but return 0 without a
+    // memory access)
+    const int32_t ny = (TSA_LAP_NOFACE_FETCH && !yin) ? 0 : 0x7FFFFFFF;
+    const int32_t nz = (TSA_LAP_NOFACE_FETCH && !zin) ? 0 : 0x7FFFFFFF;
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc((void *)yf_prev, (short)0, ny, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rzr = __builtin_amdgcn_make_buffer_rsrc((void *)zf_prev, (short)0, nz, 0x00020000);
     auto bl16 = [&](__amdgpu_buffer_rsrc_t r, uint32_t off) -> u64x2 {
       if constexpr (SYS)  // 17: sc0 sc1 (system scope, as the 8-byte loads of the split)
         return __builtin_bit_cast(u64x2, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 17));

@@ -102,3 +102,28 @@ def test_lap_residency_sgpr_cap(tsa, meta, M, NW):
     # the edge the guide names: 97-112 SGPRs leave 6 waves per SIMD, 7 below it
     assert sgpr_waves(106) == 6 and sgpr_waves(80) == 8
     assert vgpr_waves(96) == 5 and vgpr_waves(80) == 6
+
+
+def test_isa_loops_counts_the_lap_step():
+    """tools/isa_loops.py (the per-step ISA census DESIGN.md 4.4 quotes) finds
+    the four-step group loop of the single-cube bench kernel
+    (lap_kernel<1,4,f16>, RTL s3) in the built object: a loop whose no-spin
+    pass issues 4 steps' worth of VALU (the cell's 17 v_pk_maximum3 per step
+    alone is 68 per pass) and at most 80 VALU per step."""
+    obj = os.path.join(PKG_DIR, "build", "lap_kernel.o")
+    if not os.path.exists(obj):
+        pytest.skip("no built lap_kernel.o (make)")
+    sys.path.insert(0, os.path.join(PKG_DIR, "tools"))
+    import isa_loops
+    ins = isa_loops.kernel_insts(isa_loops.disassemble(obj), "lap_kernelILi1ELi4ELb1ELb0ELb0ELb0ELb0ELb0E")
+    assert ins, "kernel not found"
+    loops = [(t, a) for a, mn, ops in ins if isa_loops.BR.match(mn)
+             for t in [isa_loops.target(ops, a)] if t is not None and t < a]
+    passes = []
+    for head, tail in loops:
+        inner = [(h, t) for h, t in loops if head < h and t < tail]
+        c = isa_loops.fast_path(ins, head, tail, inner)
+        if c["valu"] and c["ds"] >= 20:  # a step loop: 6+ LDS ops per step
+            passes.append(c)
+    group = [c for c in passes if 4 * 60 <= c["valu"] <= 4 * 80]
+    assert group, passes
