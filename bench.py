@@ -285,8 +285,11 @@ def profile_child_main(args) -> int:
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    # defaults: 20 timed steps after 10 warm-ups (~0.15 s of GPU): the first
+    # launches of a fresh process run 5-25 % slow while the clocks settle
+    # (per-dispatch trace: 5.84, 5.26, 5.05, 4.85, 4.78 ms, then 4.6-4.7)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", choices=["batch", "single"], default="batch")
     ap.add_argument("--kernel", choices=["auto", "plane", "pencil"], default="auto")
     ap.add_argument("--per-gpu", type=int, default=512)
